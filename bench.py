@@ -1,0 +1,236 @@
+"""Headline benchmark: consensus rounds/s at 8192 agents x 2^20 params.
+
+One step = one synchronous gossip round X <- W X over all agents (FedLCon's
+inner step, DIST/simulators.py:190-196), W = communication_graph("circle",
+"stochastic", 8192) seeded 2028 (the reference's own construction, ring
+kernel).  Inputs are synthetic fp32 (randn), resident in HBM before timing.
+
+  python bench.py [--gpus N --steps K --warmup W]
+  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Strong scaling: the 8192 agents are split into contiguous blocks, one per
+rank; each round exchanges the two boundary rows with the neighbouring ranks
+(RCCL send/recv) while the interior rows are mixed.
+
+Rank 0 prints ONE JSON line.  `roofline` prices the dominant kernel (the
+ring mix) from HIP events around every launch in the timed region;
+`cpu_baseline` times the reference-structured torch-CPU round
+(oracle/ref_cpu.py) on this host on a bounded sample (N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "distributed-optimization-and-learning_amd")
+for _p in (ROOT, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "consensus rounds/sec at 8192 agents x 1M params (1/8 GPU) + % of HBM peak"
+HBM_PEAK_GBPS = 8000.0  # MI355X spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--agents", type=int, default=8192)
+    ap.add_argument("--params", type=int, default=1 << 20)
+    ap.add_argument("--cpu-agents", type=int, default=256, help="CPU baseline sample size (agents)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline (profiling runs)")
+    ap.add_argument("--no-copy", action="store_true", help="skip the copy-kernel calibration")
+    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_ring_8192x1M.json"))
+    return ap.parse_args()
+
+
+def ring_weights(n: int):
+    """W = communication_graph('circle', 'stochastic', n) after manual_seed(2028)."""
+    from dolhip import graph as G
+    torch.manual_seed(2028)
+    W = G.communication_graph("circle", "stochastic", n)[0]
+    rw = G.csr_from_dense(W).ring_weights()
+    assert rw is not None
+    return rw
+
+
+def copy_peak(device, gib: float = 2.0, reps: int = 10) -> float:
+    from dolhip import ops
+    n = int(gib * (1 << 30) / 4)
+    a = torch.empty(n, dtype=torch.float32, device=device).normal_()
+    b = torch.empty_like(a)
+    for _ in range(2):
+        ops.stream_copy(a, b)
+    torch.cuda.synchronize(device)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        ops.stream_copy(a, b)
+    e.record()
+    torch.cuda.synchronize(device)
+    sec = s.elapsed_time(e) / 1e3 / reps
+    del a, b
+    torch.cuda.empty_cache()
+    return 2 * n * 4 / sec / 1e9
+
+
+def cpu_baseline(n_agents: int, P: int, seconds: float, full_agents: int):
+    from oracle import ref_cpu
+    threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16)
+    torch.set_num_threads(threads)
+    torch.manual_seed(2028)
+    from dolhip import graph as G
+    W = G.communication_graph("circle", "stochastic", n_agents)[0]
+    X = torch.randn(n_agents, P)
+    rounds, sec = ref_cpu.time_rounds(W, X, min_seconds=seconds)
+    rate = rounds / sec
+    # per-byte extrapolation to the metric's 8192-agent system (optimistic for
+    # the reference: its O(N^2) neighbour scan grows faster than linearly)
+    value = rate * n_agents / full_agents
+    return {
+        "value": value,
+        "unit": "rounds/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": (f"reference-structured torch-CPU round (Neighbors scan + consensus + load_state_dict, "
+                   f"oracle/ref_cpu.py) on {n_agents} agents x {P} params, circle/stochastic: {rounds} rounds "
+                   f"in {sec:.2f} s = {rate:.3f} rounds/s; value = that x {n_agents}/{full_agents} "
+                   f"(per-byte extrapolation to {full_agents} agents)"),
+    }
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if rank == 0:
+            print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+
+    import dolhip
+    from dolhip.parallel import ShardedRing
+
+    dolhip.lib()
+    N, P = args.agents, args.params
+    wp, wn = ring_weights(N)
+    ring = ShardedRing(N, P, wp, wn, device)
+    g = torch.Generator(device=device).manual_seed(2028 + rank)
+    ring.x.normal_(generator=g)
+    ring.y.zero_()
+
+    for _ in range(args.warmup):
+        ring.step()
+    torch.cuda.synchronize(device)
+
+    # kernel events: around every launch of the dominant kernel
+    K = args.steps
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    ring.kernel_events = []
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for k in range(K):
+        if world == 1:
+            ev[k][0].record()
+            ring.step()
+            ev[k][1].record()
+        else:
+            ring.kernel_events = ev[k]
+            ring.step()
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    kern_rows = ring.n_local if world == 1 else ring.n_local - 2
+    alg_bytes = 2 * kern_rows * P * 4  # each row read once + written once
+    achieved = alg_bytes / (kern_ms / 1e3) / 1e9
+
+    copy_gbps = None
+    if not args.no_copy:
+        del ring.y
+        torch.cuda.empty_cache()
+        copy_gbps = copy_peak(device)
+
+    traffic = None
+    traffic_src = None
+    if os.path.exists(args.traffic_file):
+        try:
+            tr = json.load(open(args.traffic_file))
+            if tr.get("agents") == N and tr.get("params") == P and tr.get("n_gpus", 1) == world:
+                traffic = tr.get("hbm_bytes_per_launch")
+                traffic_src = os.path.relpath(args.traffic_file, ROOT)
+        except (OSError, ValueError):
+            traffic = None
+
+    out = None
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu:
+            cpu = cpu_baseline(args.cpu_agents, P, args.cpu_seconds, N)
+        value = K / elapsed
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "rounds/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / K * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (randn agent parameters, seed 2028)",
+            "config": {
+                "workload": f"ring gossip mix X <- W X, {N} agents x {P} params, W = "
+                            f"communication_graph('circle','stochastic',{N}) seed 2028",
+                "agents": N,
+                "params": P,
+                "topology": "circle",
+                "mode": "stochastic",
+                "parallelism": f"agent-shard x{world}" + (" + RCCL halo send/recv" if world > 1 else ""),
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "ring_mix_kernel",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBPS,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
+                "algorithmic_bytes_per_launch": alg_bytes,
+                "kernel_ms": kern_ms,
+                "copy_kernel_GBps": copy_gbps,
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,673 @@
+// dol_hip.hip — gfx950 kernels and the C-ABI of include/dol_hip.h.
+//
+// Build (see csrc/Makefile):  hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fPIC -shared
+// -ffp-contract=off is load-bearing: the reference (torch CPU) rounds every
+// product and every sum separately in the mixing / dual / prox arithmetic, so
+// the only fused multiply-add in this file is the explicit __builtin_fmaf of
+// the SGD parameter update (ATen's vectorised add_(d, alpha=-lr) is an FMA).
+//
+// Layout: agent k's parameter vector is row k of a row-major fp32 matrix
+// with leading dimension ld (elements).  Columns are streamed 16 B per lane
+// (f4) when every row base is 16-B aligned; otherwise, and for the
+// P % 4 tail, the same kernels run on scalar columns.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <stdarg.h>
+#include <algorithm>
+
+#include "../../include/dol_hip.h"
+
+namespace {
+
+// ----------------------------------------------------------------------------
+// error plumbing
+// ----------------------------------------------------------------------------
+thread_local char g_err[512] = "";
+
+int fail(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    return fail(-static_cast<int>(e), "%s: launch failed: %s", what, hipGetErrorString(e));
+  }
+  g_err[0] = '\0';
+  return DOL_OK;
+}
+
+constexpr int kThreads = 256;            // 4 waves of 64
+constexpr int64_t kMaxBlocks = int64_t(1) << 24;
+
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  if (!v || !*v) return dflt;
+  return atoi(v);
+}
+
+// ----------------------------------------------------------------------------
+// vector helpers: the same kernel body runs on float (tail / unaligned) and
+// f4 (main stream).  All arithmetic is explicit per lane so that each
+// product and sum rounds once, exactly as the reference's torch CPU ops.
+// ----------------------------------------------------------------------------
+typedef float f4 __attribute__((ext_vector_type(4)));  // native 16-B vector (nontemporal builtins need it)
+
+template <typename V> struct Vec;
+template <> struct Vec<float> {
+  static constexpr int W = 1;
+};
+template <> struct Vec<f4> {
+  static constexpr int W = 4;
+};
+
+__device__ __forceinline__ float axpy0(float wp, float a, float wn, float b) {
+  // ((+0 + wp*a) + wn*b) with every operation rounded (no contraction)
+  float acc = 0.0f;
+  acc = acc + wp * a;
+  acc = acc + wn * b;
+  return acc;
+}
+__device__ __forceinline__ f4 axpy0(float wp, f4 a, float wn, f4 b) {
+  return f4{axpy0(wp, a.x, wn, b.x), axpy0(wp, a.y, wn, b.y),
+            axpy0(wp, a.z, wn, b.z), axpy0(wp, a.w, wn, b.w)};
+}
+__device__ __forceinline__ float fmac(float acc, float a, float x) { return acc + a * x; }
+__device__ __forceinline__ f4 fmac(f4 acc, float a, f4 x) {
+  return f4{acc.x + a * x.x, acc.y + a * x.y, acc.z + a * x.z, acc.w + a * x.w};
+}
+__device__ __forceinline__ float vzero(float) { return 0.0f; }
+__device__ __forceinline__ f4 vzero(f4) { return f4{0.f, 0.f, 0.f, 0.f}; }
+__device__ __forceinline__ float vadd(float a, float b) { return a + b; }
+__device__ __forceinline__ f4 vadd(f4 a, f4 b) {
+  return f4{a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w};
+}
+__device__ __forceinline__ float vdiv(float a, float s) { return a / s; }
+__device__ __forceinline__ f4 vdiv(f4 a, float s) {
+  return f4{a.x / s, a.y / s, a.z / s, a.w / s};
+}
+
+template <typename V, bool NT>
+__device__ __forceinline__ V ldv(const V* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <typename V, bool NT>
+__device__ __forceinline__ void stv(V* p, V v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
+// ----------------------------------------------------------------------------
+// Ring mix: one workgroup = one column tile (256 lanes x V) x R consecutive
+// agent rows.  The three-point stencil along the agent axis is carried in a
+// register window, so each X row segment is read once per workgroup and each
+// Y row segment written once: (R+2)/R reads, 1 write.  PF rows are loaded
+// one iteration ahead so every lane keeps PF loads in flight.
+// ----------------------------------------------------------------------------
+template <typename V, int PF, bool NT_LOAD, bool NT_STORE>
+__global__ __launch_bounds__(kThreads) void ring_mix_kernel(
+    const float* __restrict__ X, int64_t ldx, float* __restrict__ Y, int64_t ldy,
+    int n_rows, int64_t c_off, int64_t ncols_v, int64_t n_col_tiles, int rows_per_block,
+    const float* __restrict__ halo_prev, const float* __restrict__ halo_next,
+    const float* __restrict__ wprev, const float* __restrict__ wnext) {
+  const int64_t b = blockIdx.x;
+  const int64_t ct = b % n_col_tiles;
+  const int rg = static_cast<int>(b / n_col_tiles);
+  const int64_t c = ct * kThreads + threadIdx.x;  // column in units of V
+  if (c >= ncols_v) return;
+  const int r0 = rg * rows_per_block;
+  const int r1 = min(r0 + rows_per_block, n_rows);
+
+  auto row = [&](int r) -> const V* {
+    const float* base = (r < 0) ? halo_prev : (r >= n_rows ? halo_next : X + int64_t(r) * ldx);
+    return reinterpret_cast<const V*>(base + c_off) + c;
+  };
+
+  V q[PF + 2];
+  q[0] = ldv<V, NT_LOAD>(row(r0 - 1));
+  q[1] = ldv<V, NT_LOAD>(row(r0));
+#pragma unroll
+  for (int k = 0; k < PF; ++k) q[2 + k] = ldv<V, NT_LOAD>(row(min(r0 + 1 + k, r1)));
+
+  for (int i = r0; i < r1; i += PF) {
+    V nx[PF];
+#pragma unroll
+    for (int k = 0; k < PF; ++k) nx[k] = ldv<V, NT_LOAD>(row(min(i + PF + 1 + k, r1)));
+#pragma unroll
+    for (int k = 0; k < PF; ++k) {
+      const int r = i + k;
+      if (r < r1) {
+        V out = axpy0(wprev[r], q[k], wnext[r], q[k + 2]);
+        stv<V, NT_STORE>(reinterpret_cast<V*>(Y + int64_t(r) * ldy + c_off) + c, out);
+      }
+    }
+    q[0] = q[PF];
+    q[1] = q[PF + 1];
+#pragma unroll
+    for (int k = 0; k < PF; ++k) q[2 + k] = nx[k];
+  }
+}
+
+// ----------------------------------------------------------------------------
+// Generic CSR mix.  Blocks are ordered row-group fastest so that all rows of
+// one column tile are in flight together: a neighbour row segment fetched
+// from HBM by one workgroup is re-read from L2 / Infinity Cache by the others.
+// ----------------------------------------------------------------------------
+template <typename V, int RPB>
+__global__ __launch_bounds__(kThreads) void csr_mix_kernel(
+    const float* __restrict__ X, int64_t ldx, float* __restrict__ Y, int64_t ldy, int n_rows,
+    int64_t c_off, int64_t ncols_v, int64_t n_row_groups, const int32_t* __restrict__ rowptr,
+    const int32_t* __restrict__ col, const float* __restrict__ val) {
+  const int64_t b = blockIdx.x;
+  const int rg = static_cast<int>(b % n_row_groups);
+  const int64_t ct = b / n_row_groups;
+  const int64_t c = ct * kThreads + threadIdx.x;
+  if (c >= ncols_v) return;
+  const int r0 = rg * RPB;
+  const int r1 = min(r0 + RPB, n_rows);
+  const V* xb = reinterpret_cast<const V*>(X + c_off) + c;
+  for (int r = r0; r < r1; ++r) {
+    const int e0 = rowptr[r];
+    const int e1 = rowptr[r + 1];
+    V acc = vzero(V{});
+    int e = e0;
+    for (; e + 4 <= e1; e += 4) {
+      const V x0 = xb[int64_t(col[e + 0]) * (ldx / Vec<V>::W)];
+      const V x1 = xb[int64_t(col[e + 1]) * (ldx / Vec<V>::W)];
+      const V x2 = xb[int64_t(col[e + 2]) * (ldx / Vec<V>::W)];
+      const V x3 = xb[int64_t(col[e + 3]) * (ldx / Vec<V>::W)];
+      acc = fmac(acc, val[e + 0], x0);
+      acc = fmac(acc, val[e + 1], x1);
+      acc = fmac(acc, val[e + 2], x2);
+      acc = fmac(acc, val[e + 3], x3);
+    }
+    for (; e < e1; ++e) acc = fmac(acc, val[e], xb[int64_t(col[e]) * (ldx / Vec<V>::W)]);
+    __builtin_nontemporal_store(acc, reinterpret_cast<V*>(Y + int64_t(r) * ldy + c_off) + c);
+  }
+}
+
+// ----------------------------------------------------------------------------
+// Fused prox / ADMM gradient term + momentum SGD.
+// MODE: 0 = no momentum, 1 = momentum first step (buf = g'), 2 = momentum.
+// ----------------------------------------------------------------------------
+template <bool THETA, bool ALPHA, int MODE, bool WRITE_G>
+__device__ __forceinline__ void prox_sgd_lane(float& w, float& bf, float& g, float th, float al,
+                                              float rho, float neg_lr, float mom) {
+  float gg = g;
+  if constexpr (THETA) {
+    float t = rho * (w - th);
+    if constexpr (ALPHA) t = al + t;
+    gg = gg + t;
+  }
+  if constexpr (WRITE_G) g = gg;
+  float d = gg;
+  if constexpr (MODE == 1) { bf = gg; d = gg; }
+  if constexpr (MODE == 2) { bf = bf * mom + gg; d = bf; }
+  w = __builtin_fmaf(neg_lr, d, w);
+}
+
+template <typename V, bool THETA, bool ALPHA, int MODE, bool WRITE_G>
+__global__ __launch_bounds__(kThreads) void prox_sgd_kernel(
+    float* __restrict__ W, int64_t ldw, float* __restrict__ B, int64_t ldb, float* __restrict__ G,
+    int64_t ldg, const float* __restrict__ theta, const float* __restrict__ A, int64_t lda,
+    float rho, float neg_lr, float mom, int64_t c_off, int64_t ncols_v, int64_t n_col_tiles) {
+  const int64_t blk = blockIdx.x;
+  const int64_t agent = blk / n_col_tiles;
+  const int64_t c = (blk % n_col_tiles) * kThreads + threadIdx.x;
+  if (c >= ncols_v) return;
+  V* wp = reinterpret_cast<V*>(W + agent * ldw + c_off) + c;
+  V* gp = reinterpret_cast<V*>(G + agent * ldg + c_off) + c;
+  V w = *wp, g = *gp;
+  V bf{}, th{}, al{};
+  if constexpr (MODE == 2) bf = *(reinterpret_cast<V*>(B + agent * ldb + c_off) + c);
+  if constexpr (THETA) th = *(reinterpret_cast<const V*>(theta + c_off) + c);
+  if constexpr (ALPHA) al = *(reinterpret_cast<const V*>(A + agent * lda + c_off) + c);
+  if constexpr (Vec<V>::W == 1) {
+    prox_sgd_lane<THETA, ALPHA, MODE, WRITE_G>(w, bf, g, th, al, rho, neg_lr, mom);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float wj = w[j], bj = bf[j], gj = g[j];
+      prox_sgd_lane<THETA, ALPHA, MODE, WRITE_G>(wj, bj, gj, th[j], al[j], rho, neg_lr, mom);
+      w[j] = wj;
+      bf[j] = bj;
+      g[j] = gj;
+    }
+  }
+  *wp = w;
+  if constexpr (WRITE_G) *gp = g;
+  if constexpr (MODE != 0) *(reinterpret_cast<V*>(B + agent * ldb + c_off) + c) = bf;
+}
+
+// ----------------------------------------------------------------------------
+// ADMM dual update alpha += rho*(w - theta), with optional per-agent
+// ||w-theta||^2 partials (fp64, fixed reduction tree -> deterministic).
+// One block = kThreads lanes x kDualIters V-columns of one agent.
+// ----------------------------------------------------------------------------
+constexpr int kDualIters = 4;
+
+__device__ __forceinline__ double block_sum_f64(double v, double* smem) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) smem[wid] = v;
+  __syncthreads();
+  double s = 0.0;
+  if (threadIdx.x == 0) {
+    for (int i = 0; i < kThreads / 64; ++i) s += smem[i];
+  }
+  return s;
+}
+
+__device__ __forceinline__ float dual_lane(float& a, float w, float th, float rho, double& r) {
+  const float d = w - th;
+  a = a + rho * d;
+  r += double(d) * double(d);
+  return d;
+}
+
+// VEC: columns [0, n4) as f4, then the (< 4) tail columns by the first
+// lanes of the agent's last chunk; !VEC: all P columns scalar.
+template <bool VEC, bool RESID>
+__global__ __launch_bounds__(kThreads) void admm_dual_kernel(
+    float* __restrict__ A, int64_t lda, const float* __restrict__ W, int64_t ldw,
+    const float* __restrict__ theta, float rho, int64_t P, int64_t n_chunks,
+    double* __restrict__ partial) {
+  __shared__ double smem[kThreads / 64];
+  const int64_t blk = blockIdx.x;
+  const int64_t agent = blk / n_chunks;
+  const int64_t chunk = blk % n_chunks;
+  float* arow = A + agent * lda;
+  const float* wrow = W + agent * ldw;
+  double r = 0.0;
+  if constexpr (VEC) {
+    const int64_t n4 = P / 4;
+#pragma unroll
+    for (int it = 0; it < kDualIters; ++it) {
+      const int64_t c = (chunk * kDualIters + it) * kThreads + threadIdx.x;
+      if (c < n4) {
+        f4* ap = reinterpret_cast<f4*>(arow) + c;
+        const f4 w = reinterpret_cast<const f4*>(wrow)[c];
+        const f4 th = reinterpret_cast<const f4*>(theta)[c];
+        f4 a = *ap;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float aj = a[j];
+          dual_lane(aj, w[j], th[j], rho, r);
+          a[j] = aj;
+        }
+        *ap = a;
+      }
+    }
+    const int64_t tail = P - 4 * n4;
+    if (chunk == n_chunks - 1 && threadIdx.x < tail) {
+      const int64_t c = 4 * n4 + threadIdx.x;
+      float a = arow[c];
+      dual_lane(a, wrow[c], theta[c], rho, r);
+      arow[c] = a;
+    }
+  } else {
+#pragma unroll
+    for (int it = 0; it < kDualIters; ++it) {
+      const int64_t c = (chunk * kDualIters + it) * kThreads + threadIdx.x;
+      if (c < P) {
+        float a = arow[c];
+        dual_lane(a, wrow[c], theta[c], rho, r);
+        arow[c] = a;
+      }
+    }
+  }
+  if constexpr (RESID) {
+    const double s = block_sum_f64(r, smem);
+    if (threadIdx.x == 0) partial[agent * n_chunks + chunk] = s;
+  }
+}
+
+// partial layout: [n_agents][n_chunks_total]; one block per agent, fixed order.
+__global__ __launch_bounds__(kThreads) void resid_reduce_kernel(const double* __restrict__ partial,
+                                                                int64_t n_chunks,
+                                                                double* __restrict__ out) {
+  __shared__ double smem[kThreads / 64];
+  const int64_t agent = blockIdx.x;
+  double v = 0.0;
+  for (int64_t i = threadIdx.x; i < n_chunks; i += kThreads) v += partial[agent * n_chunks + i];
+  const double s = block_sum_f64(v, smem);
+  if (threadIdx.x == 0) out[agent] = s;
+}
+
+// ----------------------------------------------------------------------------
+// Ordered sum / mean over gathered rows: acc = w[o0]; acc += w[o1]; ...
+// Column-parallel; the row loop is unrolled so 8 row loads are in flight.
+// ----------------------------------------------------------------------------
+template <typename V>
+__global__ __launch_bounds__(kThreads) void ordered_sum_kernel(
+    const float* __restrict__ W, int64_t ldw, const int32_t* __restrict__ order, int m,
+    int64_t c_off, int64_t ncols_v, const float* __restrict__ acc_in, float* __restrict__ out,
+    float scale, int do_div) {
+  const int64_t c = int64_t(blockIdx.x) * kThreads + threadIdx.x;
+  if (c >= ncols_v) return;
+  const V* wb = reinterpret_cast<const V*>(W + c_off) + c;
+  const int64_t ldv = ldw / Vec<V>::W;
+  V acc;
+  int k;
+  if (acc_in) {
+    acc = *(reinterpret_cast<const V*>(acc_in + c_off) + c);
+    k = 0;
+  } else {
+    acc = wb[int64_t(order[0]) * ldv];
+    k = 1;
+  }
+  for (; k + 8 <= m; k += 8) {
+    V x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) x[u] = wb[int64_t(order[k + u]) * ldv];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc = vadd(acc, x[u]);
+  }
+  for (; k < m; ++k) acc = vadd(acc, wb[int64_t(order[k]) * ldv]);
+  if (do_div) acc = vdiv(acc, scale);
+  *(reinterpret_cast<V*>(out + c_off) + c) = acc;
+}
+
+template <typename V>
+__global__ __launch_bounds__(kThreads) void copy_kernel(const V* __restrict__ src, V* __restrict__ dst,
+                                                        int64_t n) {
+  const int64_t stride = int64_t(gridDim.x) * kThreads;
+  for (int64_t i = int64_t(blockIdx.x) * kThreads + threadIdx.x; i < n; i += stride) {
+    __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+  }
+}
+
+// ----------------------------------------------------------------------------
+// host-side launch helpers
+// ----------------------------------------------------------------------------
+inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// Split [0, P) into a f4 part and a scalar tail; returns whether the
+// f4 path is legal for all given (base, ld) pairs.
+struct ColSplit {
+  bool vec;
+  int64_t n4;    // f4 columns
+  int64_t tail;  // scalar columns after 4*n4 (or all P when !vec)
+};
+
+inline ColSplit split_cols(int64_t P, bool vec_ok) {
+  if (!vec_ok) return {false, 0, P};
+  return {true, P / 4, P % 4};
+}
+
+inline bool row_vec_ok(const void* base, int64_t ld) { return base == nullptr || (aligned16(base) && (ld % 4) == 0); }
+
+template <typename V, int PF, bool NTL, bool NTS>
+void launch_ring(const float* X, int64_t ldx, float* Y, int64_t ldy, int n_rows, int64_t c_off,
+                 int64_t ncols_v, int rpb, const float* hp, const float* hn, const float* wp,
+                 const float* wn, hipStream_t s) {
+  const int64_t n_col_tiles = cdiv(ncols_v, kThreads);
+  const int64_t n_rg = cdiv(n_rows, rpb);
+  const int64_t grid = n_col_tiles * n_rg;
+  hipLaunchKernelGGL((ring_mix_kernel<V, PF, NTL, NTS>), dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, s, X,
+                     ldx, Y, ldy, n_rows, c_off, ncols_v, n_col_tiles, rpb, hp, hn, wp, wn);
+}
+
+template <typename V>
+void launch_ring_variant(int pf, int nt, const float* X, int64_t ldx, float* Y, int64_t ldy,
+                         int n_rows, int64_t c_off, int64_t ncols_v, int rpb, const float* hp,
+                         const float* hn, const float* wp, const float* wn, hipStream_t s) {
+  // nt bit0 = nontemporal loads, bit1 = nontemporal stores
+#define DOL_RING_CASE(PFV, NTL, NTS)                                                         \
+  if (pf == PFV && nt == (NTL + 2 * NTS)) {                                                \
+    launch_ring<V, PFV, NTL, NTS>(X, ldx, Y, ldy, n_rows, c_off, ncols_v, rpb, hp, hn, wp, wn, s); \
+    return;                                                                                \
+  }
+  DOL_RING_CASE(2, 0, 1)
+  DOL_RING_CASE(4, 0, 1)
+  DOL_RING_CASE(8, 0, 1)
+  DOL_RING_CASE(4, 0, 0)
+  DOL_RING_CASE(4, 1, 1)
+  DOL_RING_CASE(8, 1, 1)
+  DOL_RING_CASE(4, 1, 0)
+#undef DOL_RING_CASE
+  launch_ring<V, 4, false, true>(X, ldx, Y, ldy, n_rows, c_off, ncols_v, rpb, hp, hn, wp, wn, s);
+}
+
+int ring_rows_per_block(int n_rows, int64_t n_col_tiles, int pf) {
+  int r = env_int("DOL_RING_ROWS", 0);
+  if (r > 0) return r;
+  r = 64;
+  // keep >= ~8 workgroups per CU (256 CUs) for small agent counts
+  while (r > pf && n_col_tiles * cdiv(n_rows, r) < 2048) r /= 2;
+  return r < 1 ? 1 : r;
+}
+
+template <typename V, int RPB>
+void launch_csr(const float* X, int64_t ldx, float* Y, int64_t ldy, int n_rows, int64_t c_off,
+                int64_t ncols_v, const int32_t* rowptr, const int32_t* col, const float* val,
+                hipStream_t s) {
+  const int64_t n_col_tiles = cdiv(ncols_v, kThreads);
+  const int64_t n_rg = cdiv(n_rows, RPB);
+  hipLaunchKernelGGL((csr_mix_kernel<V, RPB>), dim3(static_cast<unsigned>(n_col_tiles * n_rg)), dim3(kThreads), 0, s,
+                     X, ldx, Y, ldy, n_rows, c_off, ncols_v, n_rg, rowptr, col, val);
+}
+
+template <typename V, bool TH, bool AL, int MODE, bool WG>
+void launch_prox(float* w, int64_t ldw, float* b, int64_t ldb, float* g, int64_t ldg,
+                 const float* th, const float* a, int64_t lda, float rho, float lr, float mom,
+                 int n_agents, int64_t c_off, int64_t ncols_v, hipStream_t s) {
+  const int64_t n_col_tiles = cdiv(ncols_v, kThreads);
+  hipLaunchKernelGGL((prox_sgd_kernel<V, TH, AL, MODE, WG>), dim3(static_cast<unsigned>(n_col_tiles * n_agents)),
+                     dim3(kThreads), 0, s, w, ldw, b, ldb, g, ldg, th, a, lda, rho, -lr, mom, c_off,
+                     ncols_v, n_col_tiles);
+}
+
+template <typename V, bool TH, bool AL, int MODE>
+void dispatch_prox_wg(bool wg, float* w, int64_t ldw, float* b, int64_t ldb, float* g, int64_t ldg,
+                      const float* th, const float* a, int64_t lda, float rho, float lr, float mom,
+                      int n, int64_t c_off, int64_t nc, hipStream_t s) {
+  if (wg) launch_prox<V, TH, AL, MODE, true>(w, ldw, b, ldb, g, ldg, th, a, lda, rho, lr, mom, n, c_off, nc, s);
+  else launch_prox<V, TH, AL, MODE, false>(w, ldw, b, ldb, g, ldg, th, a, lda, rho, lr, mom, n, c_off, nc, s);
+}
+
+template <typename V, bool TH, bool AL>
+void dispatch_prox_mode(int mode, bool wg, float* w, int64_t ldw, float* b, int64_t ldb, float* g,
+                        int64_t ldg, const float* th, const float* a, int64_t lda, float rho,
+                        float lr, float mom, int n, int64_t c_off, int64_t nc, hipStream_t s) {
+  if (mode == 0) dispatch_prox_wg<V, TH, AL, 0>(wg, w, ldw, b, ldb, g, ldg, th, a, lda, rho, lr, mom, n, c_off, nc, s);
+  else if (mode == 1) dispatch_prox_wg<V, TH, AL, 1>(wg, w, ldw, b, ldb, g, ldg, th, a, lda, rho, lr, mom, n, c_off, nc, s);
+  else dispatch_prox_wg<V, TH, AL, 2>(wg, w, ldw, b, ldb, g, ldg, th, a, lda, rho, lr, mom, n, c_off, nc, s);
+}
+
+template <typename V>
+void dispatch_prox(bool th, bool al, int mode, bool wg, float* w, int64_t ldw, float* b,
+                   int64_t ldb, float* g, int64_t ldg, const float* tp, const float* ap,
+                   int64_t lda, float rho, float lr, float mom, int n, int64_t c_off, int64_t nc,
+                   hipStream_t s) {
+  if (!th) dispatch_prox_mode<V, false, false>(mode, wg, w, ldw, b, ldb, g, ldg, tp, ap, lda, rho, lr, mom, n, c_off, nc, s);
+  else if (!al) dispatch_prox_mode<V, true, false>(mode, wg, w, ldw, b, ldb, g, ldg, tp, ap, lda, rho, lr, mom, n, c_off, nc, s);
+  else dispatch_prox_mode<V, true, true>(mode, wg, w, ldw, b, ldb, g, ldg, tp, ap, lda, rho, lr, mom, n, c_off, nc, s);
+}
+
+}  // namespace
+
+// ============================================================================
+// C-ABI
+// ============================================================================
+extern "C" {
+
+int dol_version(void) { return 100; }
+
+const char* dol_last_error(void) { return g_err; }
+
+int dol_mix_csr_f32(const float* X, int64_t ldx, int32_t x_rows, float* Y, int64_t ldy,
+                    int32_t n_rows, int64_t P, const int32_t* rowptr, const int32_t* col,
+                    const float* val, hipStream_t s) {
+  if (n_rows < 0 || P < 0 || x_rows < 0) return fail(DOL_EINVAL, "dol_mix_csr_f32: negative size");
+  if (n_rows == 0 || P == 0) { g_err[0] = '\0'; return DOL_OK; }
+  if (!X || !Y || !rowptr || (!col && x_rows > 0) || (!val && x_rows > 0))
+    return fail(DOL_EINVAL, "dol_mix_csr_f32: null pointer");
+  if (ldx < P || ldy < P) return fail(DOL_EINVAL, "dol_mix_csr_f32: ld < P");
+  if (X == Y) return fail(DOL_EINVAL, "dol_mix_csr_f32: X and Y alias (Jacobi mix needs two buffers)");
+  const bool vec_ok = row_vec_ok(X, ldx) && row_vec_ok(Y, ldy);
+  const ColSplit cs = split_cols(P, vec_ok);
+  constexpr int RPB = 16;
+  if (cdiv(cs.n4, kThreads) * cdiv(n_rows, RPB) > kMaxBlocks)
+    return fail(DOL_EINVAL, "dol_mix_csr_f32: problem too large for one launch");
+  if (cs.n4 > 0) launch_csr<f4, RPB>(X, ldx, Y, ldy, n_rows, 0, cs.n4, rowptr, col, val, s);
+  if (cs.tail > 0)
+    launch_csr<float, RPB>(X, ldx, Y, ldy, n_rows, cs.n4 * 4, cs.tail, rowptr, col, val, s);
+  return check_launch("dol_mix_csr_f32");
+}
+
+int dol_mix_ring_f32(const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t n_rows, int64_t P,
+                     const float* halo_prev, const float* halo_next, const float* w_prev,
+                     const float* w_next, hipStream_t s) {
+  if (n_rows < 0 || P < 0) return fail(DOL_EINVAL, "dol_mix_ring_f32: negative size");
+  if (n_rows == 0 || P == 0) { g_err[0] = '\0'; return DOL_OK; }
+  if (!X || !Y || !w_prev || !w_next) return fail(DOL_EINVAL, "dol_mix_ring_f32: null pointer");
+  if (ldx < P || ldy < P) return fail(DOL_EINVAL, "dol_mix_ring_f32: ld < P");
+  if (X == Y) return fail(DOL_EINVAL, "dol_mix_ring_f32: X and Y alias (Jacobi mix needs two buffers)");
+  if ((halo_prev == nullptr) != (halo_next == nullptr))
+    return fail(DOL_EINVAL, "dol_mix_ring_f32: pass both halos or neither");
+  if (!halo_prev) {
+    if (n_rows < 3) return fail(DOL_EINVAL, "dol_mix_ring_f32: wrap-around ring needs n_rows >= 3");
+    halo_prev = X + int64_t(n_rows - 1) * ldx;
+    halo_next = X;
+  }
+  const bool vec_ok = row_vec_ok(X, ldx) && row_vec_ok(Y, ldy) && aligned16(halo_prev) && aligned16(halo_next);
+  const ColSplit cs = split_cols(P, vec_ok);
+  const int pf = env_int("DOL_RING_PF", 4);
+  const int nt = env_int("DOL_RING_NT", 2);
+  if (cs.n4 > 0) {
+    const int rpb = ring_rows_per_block(n_rows, cdiv(cs.n4, kThreads), pf);
+    if (cdiv(cs.n4, kThreads) * cdiv(n_rows, rpb) > kMaxBlocks)
+      return fail(DOL_EINVAL, "dol_mix_ring_f32: problem too large for one launch");
+    launch_ring_variant<f4>(pf, nt, X, ldx, Y, ldy, n_rows, 0, cs.n4, rpb, halo_prev, halo_next, w_prev, w_next, s);
+  }
+  if (cs.tail > 0) {
+    const int rpb = ring_rows_per_block(n_rows, cdiv(cs.tail, kThreads), 4);
+    if (cdiv(cs.tail, kThreads) * cdiv(n_rows, rpb) > kMaxBlocks)
+      return fail(DOL_EINVAL, "dol_mix_ring_f32: problem too large for one launch");
+    launch_ring<float, 4, false, true>(X, ldx, Y, ldy, n_rows, cs.n4 * 4, cs.tail, rpb, halo_prev, halo_next,
+                                       w_prev, w_next, s);
+  }
+  return check_launch("dol_mix_ring_f32");
+}
+
+int dol_prox_admm_sgd_f32(float* w, int64_t ldw, float* buf, int64_t ldb, float* g, int64_t ldg,
+                          const float* theta, const float* alpha, int64_t lda, float rho, float lr,
+                          float momentum, int first_step, int write_grad, int32_t n_agents,
+                          int64_t P, hipStream_t s) {
+  if (n_agents < 0 || P < 0) return fail(DOL_EINVAL, "dol_prox_admm_sgd_f32: negative size");
+  if (n_agents == 0 || P == 0) { g_err[0] = '\0'; return DOL_OK; }
+  if (!w || !g) return fail(DOL_EINVAL, "dol_prox_admm_sgd_f32: null w or g");
+  if (alpha && !theta) return fail(DOL_EINVAL, "dol_prox_admm_sgd_f32: alpha without theta");
+  const int mode = (momentum == 0.0f) ? 0 : (first_step ? 1 : 2);
+  if (mode != 0 && !buf) return fail(DOL_EINVAL, "dol_prox_admm_sgd_f32: momentum needs buf");
+  if (ldw < P || ldg < P || (mode != 0 && ldb < P) || (alpha && lda < P))
+    return fail(DOL_EINVAL, "dol_prox_admm_sgd_f32: ld < P");
+  const bool vec_ok = row_vec_ok(w, ldw) && row_vec_ok(g, ldg) && (mode == 0 || row_vec_ok(buf, ldb)) &&
+                      row_vec_ok(theta, 0) && row_vec_ok(alpha, alpha ? lda : 0);
+  const ColSplit cs = split_cols(P, vec_ok);
+  if (cdiv(cs.n4 + cs.tail, kThreads) * n_agents > kMaxBlocks)
+    return fail(DOL_EINVAL, "dol_prox_admm_sgd_f32: problem too large for one launch");
+  const bool th = theta != nullptr, al = alpha != nullptr, wg = write_grad != 0;
+  if (cs.n4 > 0)
+    dispatch_prox<f4>(th, al, mode, wg, w, ldw, buf, ldb, g, ldg, theta, alpha, lda, rho, lr,
+                          momentum, n_agents, 0, cs.n4, s);
+  if (cs.tail > 0)
+    dispatch_prox<float>(th, al, mode, wg, w, ldw, buf, ldb, g, ldg, theta, alpha, lda, rho, lr,
+                         momentum, n_agents, cs.n4 * 4, cs.tail, s);
+  return check_launch("dol_prox_admm_sgd_f32");
+}
+
+int64_t dol_admm_dual_workspace_bytes(int32_t n_agents, int64_t P) {
+  if (n_agents <= 0 || P <= 0) return 0;
+  // the scalar path has the most chunks: cdiv(P, kThreads*kDualIters)
+  return int64_t(n_agents) * cdiv(P, int64_t(kThreads) * kDualIters) * int64_t(sizeof(double));
+}
+
+int dol_admm_dual_f32(float* alpha, int64_t lda, const float* w, int64_t ldw, const float* theta,
+                      float rho, int32_t n_agents, int64_t P, double* resid_sq, void* work,
+                      hipStream_t s) {
+  if (n_agents < 0 || P < 0) return fail(DOL_EINVAL, "dol_admm_dual_f32: negative size");
+  if (n_agents == 0) { g_err[0] = '\0'; return DOL_OK; }
+  if (P > 0 && (!alpha || !w || !theta)) return fail(DOL_EINVAL, "dol_admm_dual_f32: null pointer");
+  if (resid_sq && !work && P > 0) return fail(DOL_EINVAL, "dol_admm_dual_f32: resid_sq needs a workspace");
+  if (lda < P || ldw < P) return fail(DOL_EINVAL, "dol_admm_dual_f32: ld < P");
+  if (P == 0) {
+    if (resid_sq) (void)hipMemsetAsync(resid_sq, 0, sizeof(double) * n_agents, s);
+    return check_launch("dol_admm_dual_f32");
+  }
+  const bool vec = row_vec_ok(alpha, lda) && row_vec_ok(w, ldw) && row_vec_ok(theta, 0);
+  const int64_t per_block = int64_t(kThreads) * kDualIters;
+  const int64_t chunks = vec ? std::max<int64_t>(1, cdiv(P / 4, per_block)) : cdiv(P, per_block);
+  if (chunks * n_agents > kMaxBlocks) return fail(DOL_EINVAL, "dol_admm_dual_f32: problem too large");
+  double* partial = static_cast<double*>(work);
+  const dim3 grid(static_cast<unsigned>(chunks * n_agents));
+  if (resid_sq) {
+    if (vec) hipLaunchKernelGGL((admm_dual_kernel<true, true>), grid, dim3(kThreads), 0, s, alpha, lda, w, ldw, theta, rho, P, chunks, partial);
+    else hipLaunchKernelGGL((admm_dual_kernel<false, true>), grid, dim3(kThreads), 0, s, alpha, lda, w, ldw, theta, rho, P, chunks, partial);
+    hipLaunchKernelGGL(resid_reduce_kernel, dim3(n_agents), dim3(kThreads), 0, s, partial, chunks, resid_sq);
+  } else {
+    if (vec) hipLaunchKernelGGL((admm_dual_kernel<true, false>), grid, dim3(kThreads), 0, s, alpha, lda, w, ldw, theta, rho, P, chunks, partial);
+    else hipLaunchKernelGGL((admm_dual_kernel<false, false>), grid, dim3(kThreads), 0, s, alpha, lda, w, ldw, theta, rho, P, chunks, partial);
+  }
+  return check_launch("dol_admm_dual_f32");
+}
+
+int dol_ordered_sum_f32(const float* W, int64_t ldw, const int32_t* order, int32_t m, int64_t P,
+                        const float* acc_in, float* acc_out, float scale, hipStream_t s) {
+  if (m < 0 || P < 0) return fail(DOL_EINVAL, "dol_ordered_sum_f32: negative size");
+  if (P == 0) { g_err[0] = '\0'; return DOL_OK; }
+  if (m == 0 && !acc_in) return fail(DOL_EINVAL, "dol_ordered_sum_f32: m == 0 needs acc_in");
+  if (!acc_out || (m > 0 && (!W || !order))) return fail(DOL_EINVAL, "dol_ordered_sum_f32: null pointer");
+  if (m > 0 && ldw < P) return fail(DOL_EINVAL, "dol_ordered_sum_f32: ld < P");
+  if (!(scale > 0.0f)) return fail(DOL_EINVAL, "dol_ordered_sum_f32: scale must be > 0");
+  const bool vec_ok = row_vec_ok(W, ldw) && row_vec_ok(acc_in, 0) && row_vec_ok(acc_out, 0);
+  const ColSplit cs = split_cols(P, vec_ok);
+  const int do_div = scale != 1.0f;
+  if (cs.n4 > 0)
+    hipLaunchKernelGGL(ordered_sum_kernel<f4>, dim3(static_cast<unsigned>(cdiv(cs.n4, kThreads))), dim3(kThreads), 0,
+                       s, W, ldw, order, m, int64_t(0), cs.n4, acc_in, acc_out, scale, do_div);
+  if (cs.tail > 0)
+    hipLaunchKernelGGL(ordered_sum_kernel<float>, dim3(static_cast<unsigned>(cdiv(cs.tail, kThreads))), dim3(kThreads), 0,
+                       s, W, ldw, order, m, cs.n4 * 4, cs.tail, acc_in, acc_out, scale, do_div);
+  return check_launch("dol_ordered_sum_f32");
+}
+
+int dol_ordered_mean_f32(const float* W, int64_t ldw, const int32_t* order, int32_t m, int64_t P,
+                         float* theta, hipStream_t s) {
+  if (m <= 0) return fail(DOL_EINVAL, "dol_ordered_mean_f32: m must be >= 1 (reference indexes w[0])");
+  if (theta == W) return fail(DOL_EINVAL, "dol_ordered_mean_f32: theta aliases W");
+  return dol_ordered_sum_f32(W, ldw, order, m, P, nullptr, theta, static_cast<float>(m), s);
+}
+
+int dol_stream_copy_f32(const float* src, float* dst, int64_t n, hipStream_t s) {
+  if (n < 0) return fail(DOL_EINVAL, "dol_stream_copy_f32: negative size");
+  if (n == 0) { g_err[0] = '\0'; return DOL_OK; }
+  if (!src || !dst) return fail(DOL_EINVAL, "dol_stream_copy_f32: null pointer");
+  const int64_t grid = 256 * 8;
+  if (aligned16(src) && aligned16(dst)) {
+    const int64_t n4 = n / 4;
+    if (n4 > 0)
+      hipLaunchKernelGGL(copy_kernel<f4>, dim3(grid), dim3(kThreads), 0, s, reinterpret_cast<const f4*>(src),
+                         reinterpret_cast<f4*>(dst), n4);
+    if (n % 4)
+      hipLaunchKernelGGL(copy_kernel<float>, dim3(1), dim3(kThreads), 0, s, src + 4 * n4, dst + 4 * n4, n % 4);
+  } else {
+    hipLaunchKernelGGL(copy_kernel<float>, dim3(grid), dim3(kThreads), 0, s, src, dst, n);
+  }
+  return check_launch("dol_stream_copy_f32");
+}
+
+}  // extern "C"

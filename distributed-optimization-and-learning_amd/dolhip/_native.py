@@ -1,0 +1,76 @@
+"""ctypes binding of libdol_hip.so (the C-ABI declared in include/dol_hip.h).
+
+The library is built in-tree (csrc/Makefile -> dolhip/libdol_hip.so) and is
+the only compute path: there is no CPU fallback.  If the library is missing
+every op raises DolNativeError.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(_HERE)
+LIB_PATH = os.path.join(_HERE, "libdol_hip.so")
+CSRC = os.path.join(PKG_ROOT, "csrc")
+HEADER = os.path.join(os.path.dirname(PKG_ROOT), "include", "dol_hip.h")
+
+
+class DolNativeError(RuntimeError):
+    """Raised when the HIP library is missing or a C-ABI call fails."""
+
+
+_c_f32p = ctypes.c_void_p  # device pointers travel as integers
+_i64 = ctypes.c_int64
+_i32 = ctypes.c_int32
+_f32 = ctypes.c_float
+_ptr = ctypes.c_void_p
+
+# name -> argtypes (restype int unless listed in _RESTYPES)
+SIGNATURES = {
+    "dol_version": [],
+    "dol_last_error": [],
+    "dol_mix_csr_f32": [_ptr, _i64, _i32, _ptr, _i64, _i32, _i64, _ptr, _ptr, _ptr, _ptr],
+    "dol_mix_ring_f32": [_ptr, _i64, _ptr, _i64, _i32, _i64, _ptr, _ptr, _ptr, _ptr, _ptr],
+    "dol_prox_admm_sgd_f32": [_ptr, _i64, _ptr, _i64, _ptr, _i64, _ptr, _ptr, _i64, _f32, _f32, _f32,
+                              ctypes.c_int, ctypes.c_int, _i32, _i64, _ptr],
+    "dol_admm_dual_f32": [_ptr, _i64, _ptr, _i64, _ptr, _f32, _i32, _i64, _ptr, _ptr, _ptr],
+    "dol_admm_dual_workspace_bytes": [_i32, _i64],
+    "dol_ordered_mean_f32": [_ptr, _i64, _ptr, _i32, _i64, _ptr, _ptr],
+    "dol_ordered_sum_f32": [_ptr, _i64, _ptr, _i32, _i64, _ptr, _ptr, _f32, _ptr],
+    "dol_stream_copy_f32": [_ptr, _ptr, _i64, _ptr],
+}
+_RESTYPES = {"dol_last_error": ctypes.c_char_p, "dol_admm_dual_workspace_bytes": ctypes.c_int64}
+
+_lib = None
+
+
+def build(force: bool = False) -> str:
+    """Compile libdol_hip.so for gfx950 with hipcc (works without a GPU)."""
+    if force or not os.path.exists(LIB_PATH):
+        subprocess.run(["make", "-s", "-C", CSRC], check=True)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise DolNativeError(
+                f"{LIB_PATH} is missing: build it with `make -C {CSRC}` (or __graft_entry__.build()); "
+                "dolhip has no CPU fallback")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, argtypes in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.argtypes = argtypes
+            fn.restype = _RESTYPES.get(name, ctypes.c_int)
+        _lib = L
+    return _lib
+
+
+def call(name: str, *args) -> None:
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        msg = lib().dol_last_error().decode(errors="replace")
+        raise DolNativeError(f"{name} returned {rc}: {msg}")

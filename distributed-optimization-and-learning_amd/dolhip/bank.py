@@ -1,0 +1,182 @@
+"""AgentBank: the stacked, HBM-resident state of N agents.
+
+The reference keeps one nn.Module per agent and "communicates" by reading
+other agents' state_dict() (DIST/simulators.py:91-97, DEC/servers.py:60-64).
+Here agent k's flattened parameters are row k of one [N, ld] fp32 matrix
+(flattening order = state_dict key order, ld = P rounded up to 64 floats so
+every row starts 256-B aligned and streams as 16-B lanes).  Each agent's
+nn.Module parameters are *views* into its row, so PyTorch-ROCm forward/
+backward and the HIP kernels see the same memory without copies.
+
+Buffers (allocated on demand):
+  x      parameters (the mixing input)          [N, ld]
+  y      mixing output (Jacobi double buffer)   [N, ld]
+  grad   per-agent gradients                    [N, ld]
+  mom    SGD momentum buffers                   [N, ld]
+  alpha  ADMM duals                             [N, ld]
+A mixing round writes y from x and then swaps the two (no copy, matching the
+reference's synchronous load_state_dict write-back, DIST/simulators.py:151-152).
+"""
+from __future__ import annotations
+
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple
+
+import torch
+
+from . import ops
+
+Layout = List[Tuple[str, Tuple[int, ...]]]
+
+ROW_ALIGN = 64  # floats (256 B)
+
+
+def layout_of(module: torch.nn.Module) -> Layout:
+    return [(k, tuple(v.shape)) for k, v in module.state_dict().items()]
+
+
+def layout_size(layout: Layout) -> int:
+    n = 0
+    for _, shape in layout:
+        c = 1
+        for s in shape:
+            c *= int(s)
+        n += c
+    return n
+
+
+def round_up(x: int, a: int) -> int:
+    return (x + a - 1) // a * a
+
+
+class AgentBank:
+    def __init__(self, n_agents: int, layout_or_P, device, ld: Optional[int] = None):
+        self.device = torch.device(device)
+        if isinstance(layout_or_P, int):
+            self.layout: Layout = [("w", (int(layout_or_P),))]
+        else:
+            self.layout = [(k, tuple(s)) for k, s in layout_or_P]
+        self.n = int(n_agents)
+        self.P = layout_size(self.layout)
+        self.ld = int(ld) if ld is not None else round_up(max(self.P, 1), ROW_ALIGN)
+        self._buf: Dict[str, torch.Tensor] = {}
+        self._modules: List[Optional[torch.nn.Module]] = [None] * self.n
+        self.offsets = []
+        off = 0
+        for k, shape in self.layout:
+            c = 1
+            for s in shape:
+                c *= int(s)
+            self.offsets.append((k, off, c, shape))
+            off += c
+
+    # ------------------------------------------------------------------ buffers
+    def buffer(self, name: str, zero: bool = False) -> torch.Tensor:
+        t = self._buf.get(name)
+        if t is None:
+            alloc = torch.zeros if zero else torch.empty
+            t = alloc(self.n, self.ld, dtype=torch.float32, device=self.device)
+            self._buf[name] = t
+        return t
+
+    @property
+    def x(self) -> torch.Tensor:
+        return self.buffer("x")
+
+    def has(self, name: str) -> bool:
+        return name in self._buf
+
+    def rows(self, name: str = "x") -> torch.Tensor:
+        """[N, P] view (without the alignment padding)."""
+        return self.buffer(name)[:, : self.P]
+
+    def row_views(self, i: int, name: str = "x") -> Dict[str, torch.Tensor]:
+        r = self.buffer(name)[i]
+        return {k: r[o:o + c].view(shape) for k, o, c, shape in self.offsets}
+
+    # ------------------------------------------------------------------ modules
+    def load_module(self, i: int, module: torch.nn.Module, name: str = "x") -> None:
+        sd = module.state_dict()
+        r = self.buffer(name)[i]
+        with torch.no_grad():
+            for k, o, c, _ in self.offsets:
+                r[o:o + c].copy_(sd[k].reshape(-1))
+
+    def bind(self, i: int, module: torch.nn.Module, grads: bool = True) -> None:
+        """Make module's parameters (and .grad) views into row i of x (grad)."""
+        self._modules[i] = module
+        self._rebind(i, grads)
+
+    def _rebind(self, i: int, grads: bool = True) -> None:
+        module = self._modules[i]
+        if module is None:
+            return
+        xv = self.row_views(i, "x")
+        gv = self.row_views(i, "grad") if grads else None
+        params = dict(module.named_parameters())
+        for k, t in module.state_dict(keep_vars=True).items():
+            if k in params:
+                p = params[k]
+                p.data = xv[k]
+                if gv is not None:
+                    p.grad = gv[k]
+            else:  # buffers (none in the reference models) are copied, not bound
+                with torch.no_grad():
+                    xv[k].copy_(t)
+
+    def rebind_all(self) -> None:
+        for i in range(self.n):
+            if self._modules[i] is not None:
+                self._rebind(i, self.has("grad"))
+
+    def state_dict(self, i: int, name: str = "x", clone: bool = True) -> Dict[str, torch.Tensor]:
+        v = self.row_views(i, name)
+        return {k: t.clone() for k, t in v.items()} if clone else v
+
+    # ------------------------------------------------------------------ mixing
+    def swap(self, a: str = "x", b: str = "y") -> None:
+        self._buf[a], self._buf[b] = self._buf[b], self._buf[a]
+        if a == "x" or b == "x":
+            self.rebind_all()
+
+    def mix(self, plan, steps: int = 1) -> None:
+        """X <- W X, `steps` times (synchronous / Jacobi rounds)."""
+        y = self.buffer("y")
+        for _ in range(steps):
+            plan.apply(self.buffer("x"), y, P=self.P)
+            self._buf["x"], self._buf["y"] = y, self._buf["x"]
+            y = self._buf["y"]
+        self.rebind_all()
+
+    # ------------------------------------------------------------------ primal / dual
+    def local_step(self, lr: float, momentum: float, first_step: bool, theta: Optional[torch.Tensor] = None,
+                   rho: float = 0.0, admm: bool = False, write_grad: bool = True,
+                   agents: Optional[slice] = None) -> None:
+        """Fused gradient term + momentum SGD on rows `agents` (default all)."""
+        sl = agents if agents is not None else slice(0, self.n)
+        x, g = self.buffer("x")[sl], self.buffer("grad")[sl]
+        buf = self.buffer("mom")[sl] if momentum != 0.0 else None
+        alpha = self.buffer("alpha", zero=True)[sl] if admm else None
+        ops.prox_admm_sgd(x, g, buf=buf, theta=theta, alpha=alpha, rho=rho, lr=lr, momentum=momentum,
+                          first_step=first_step, write_grad=write_grad, P=self.P)
+
+    def dual_update(self, theta: torch.Tensor, rho: float, resid_sq: Optional[torch.Tensor] = None,
+                    agents: Optional[slice] = None) -> None:
+        sl = agents if agents is not None else slice(0, self.n)
+        ops.admm_dual(self.buffer("alpha", zero=True)[sl], self.buffer("x")[sl], theta, rho,
+                      resid_sq=resid_sq, P=self.P)
+
+    def ordered_mean(self, order: Sequence[int], out: Optional[torch.Tensor] = None,
+                     name: str = "x") -> torch.Tensor:
+        idx = torch.as_tensor(list(order), dtype=torch.int32, device=self.device)
+        return ops.ordered_mean(self.buffer(name), idx, out=out, P=self.P)
+
+    def unflatten(self, vec: torch.Tensor) -> Dict[str, torch.Tensor]:
+        return {k: vec[o:o + c].view(shape) for k, o, c, shape in self.offsets}
+
+    def flatten(self, sd: Dict[str, torch.Tensor], out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        if out is None:
+            out = torch.empty(self.P, dtype=torch.float32, device=self.device)
+        with torch.no_grad():
+            for k, o, c, _ in self.offsets:
+                out[o:o + c].copy_(sd[k].reshape(-1))
+        return out

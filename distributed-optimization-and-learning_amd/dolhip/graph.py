@@ -1,0 +1,248 @@
+"""Mixing-matrix construction and its device form (CSR / ring plan).
+
+`communication_graph` reproduces Simulator.communication_graph
+(DIST/simulators.py:40-86) value-for-value, including how much of the global
+torch RNG it consumes (one torch.rand(n, n) for either weighted mode, drawn
+after model init in Simulator.__init__, :19-22), so seeded runs build the
+same W as the reference.  Differences, all opt-in or failure-only:
+  * the Sinkhorn loop of "double_stochastic" (:80-84) is bounded: it raises
+    SinkhornNotConverged after `sinkhorn_max_iters` sweeps instead of hanging
+    (SURVEY.md section 7 lists seeds/sizes where the reference never returns),
+    and `sinkhorn_tol` > 0 accepts max|sum-1| <= tol;
+  * "complete" is accepted as an alias of the reference's spelling "compelete".
+
+`csr_from_dense` is Simulator.Neighbors (:91-97) for every row at once:
+ascending j, keep W[i][j] > 0 (so NaN and non-positive weights drop out).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Union
+
+import numpy as np
+import torch
+
+Graph = Union[torch.Tensor, np.ndarray]
+
+TOPOLOGIES = ("circle", "star", "compelete", "dynamic")
+
+
+class SinkhornNotConverged(RuntimeError):
+    pass
+
+
+def adjacency(topology: str, n: int) -> List[np.ndarray]:
+    """0/1 float64 adjacency list (one entry, or n for 'dynamic')."""
+    topology = "compelete" if topology == "complete" else topology
+    if topology == "circle":
+        a = np.zeros((n, n))
+        idx = np.arange(n)
+        a[idx, (idx + 1) % n] = 1.0
+        a[(idx + 1) % n, idx] = 1.0
+        return [a]
+    if topology == "star":
+        a = np.zeros((n, n))
+        a[1:, 0] = 1.0
+        a[0, 1:] = 1.0
+        return [a]
+    if topology == "compelete":
+        a = np.ones((n, n))
+        np.fill_diagonal(a, 0.0)
+        return [a]
+    if topology == "dynamic":
+        out = []
+        for t in range(n):
+            a = np.zeros((n, n))
+            a[t, (t + 1) % n] = 1.0
+            a[(t + 1) % n, t] = 1.0
+            out.append(a)
+        return out
+    return []  # the reference silently builds no graph for an unknown topology
+
+
+def _column_stochastic_T(rand: torch.Tensor, a: np.ndarray) -> torch.Tensor:
+    # G = R o A; normalise columns; W = G^T, so row i holds agent i's weights
+    g = rand * torch.tensor(a).int().float()
+    g /= g.sum(0)
+    return g.T
+
+
+def _sinkhorn(g: np.ndarray, max_iters: int, tol: float) -> np.ndarray:
+    def done(x):
+        r, c = x.sum(1), x.sum(0)
+        if tol > 0:
+            return max(np.max(np.abs(r - 1)), np.max(np.abs(c - 1))) <= tol
+        return not ((np.any(r != 1)) | (np.any(c != 1)))
+
+    it = 0
+    while not done(g):
+        if it >= max_iters:
+            raise SinkhornNotConverged(
+                f"double_stochastic: row/column sums not exactly 1 after {max_iters} sweeps "
+                "(the reference loops forever here); pass sinkhorn_tol > 0 to accept a tolerance")
+        g /= g.sum(0)
+        g = g / g.sum(1)[:, np.newaxis]
+        it += 1
+    return g
+
+
+def communication_graph(topology: str, mode: str, n: int, sinkhorn_max_iters: int = 100_000,
+                        sinkhorn_tol: float = 0.0, verbose: bool = False) -> List[Graph]:
+    """Mixing matrices W[t] (row i = weights agent i puts on its neighbours).
+
+    stochastic         -> list of fp32 torch tensors (rows sum to 1)
+    double_stochastic  -> list of fp32 torch tensors (Sinkhorn, bounded)
+    anything else      -> list of raw 0/1 float64 numpy adjacencies
+    """
+    graphs: List[Graph] = list(adjacency(topology, n))
+    if mode == "stochastic":
+        rand = torch.rand(n, n)
+        graphs = [_column_stochastic_T(rand, a) for a in graphs]
+    elif mode == "double_stochastic":
+        rand = torch.rand(n, n)
+        if topology == "star":
+            rand = torch.ones(n, n) / n
+        out = []
+        for a in graphs:
+            g = np.array(rand * torch.tensor(a).int().float())
+            if verbose:
+                print(g.sum(1), g.sum(0))
+            out.append(torch.tensor(_sinkhorn(g, sinkhorn_max_iters, sinkhorn_tol)).T)
+        graphs = out
+    return graphs
+
+
+@dataclass
+class CSR:
+    """Host CSR of a mixing matrix (int32 rowptr/col, fp32 val)."""
+
+    n_rows: int
+    n_cols: int
+    rowptr: np.ndarray
+    col: np.ndarray
+    val: np.ndarray
+
+    @property
+    def nnz(self) -> int:
+        return int(self.col.size)
+
+    def ring_weights(self):
+        """(w_prev, w_next) if every row i is exactly {i-1, i+1} (mod n), n >= 3."""
+        n = self.n_rows
+        if n < 3 or self.n_cols != n or self.nnz != 2 * n:
+            return None
+        if not np.all(np.diff(self.rowptr) == 2):
+            return None
+        i = np.arange(n)
+        prev, nxt = (i - 1) % n, (i + 1) % n
+        c0, c1 = self.col[0::2], self.col[1::2]
+        lo, hi = np.minimum(prev, nxt), np.maximum(prev, nxt)
+        if not (np.array_equal(c0, lo) and np.array_equal(c1, hi)):
+            return None
+        v0, v1 = self.val[0::2], self.val[1::2]
+        w_prev = np.where(prev < nxt, v0, v1).astype(np.float32)
+        w_next = np.where(prev < nxt, v1, v0).astype(np.float32)
+        return w_prev, w_next
+
+    def dense(self) -> np.ndarray:
+        d = np.zeros((self.n_rows, self.n_cols), np.float32)
+        for i in range(self.n_rows):
+            s, e = self.rowptr[i], self.rowptr[i + 1]
+            d[i, self.col[s:e]] = self.val[s:e]
+        return d
+
+
+def csr_from_dense(W: Graph) -> CSR:
+    """Neighbors (DIST/simulators.py:91-97) for all rows: j ascending, W[i][j] > 0."""
+    Wn = W.detach().cpu().numpy() if isinstance(W, torch.Tensor) else np.asarray(W)
+    if Wn.ndim != 2:
+        raise ValueError("W must be 2-D")
+    n, m = Wn.shape
+    with np.errstate(invalid="ignore"):
+        mask = Wn > 0
+    rows, cols = np.nonzero(mask)  # row-major: ascending j within each row
+    counts = np.bincount(rows, minlength=n)
+    rowptr = np.zeros(n + 1, np.int64)
+    np.cumsum(counts, out=rowptr[1:])
+    if rowptr[-1] > np.iinfo(np.int32).max:
+        raise ValueError("too many nonzeros for int32 CSR")
+    return CSR(n, m, rowptr.astype(np.int32), cols.astype(np.int32),
+               Wn[rows, cols].astype(np.float32))
+
+
+def random_regular_csr(n: int, degree: int = 4, seed: int = 2028) -> CSR:
+    """Seeded simple random d-regular graph (union of d/2 random Hamiltonian
+    cycles, resampled until simple) with the reference's 'stochastic' weight
+    rule: G = R o A, columns normalised, W = G^T.  Not in the reference; the
+    synthetic mixing workload of BASELINE config 3."""
+    if degree % 2 or degree < 2 or n <= degree:
+        raise ValueError("need an even degree 2 <= d < n")
+    gen = torch.Generator().manual_seed(seed)
+    for _ in range(1000):
+        edges = set()
+        simple = True
+        for _k in range(degree // 2):
+            perm = torch.randperm(n, generator=gen).numpy()
+            for a, b in zip(perm, np.roll(perm, -1)):
+                e = (min(a, b), max(a, b))
+                if e in edges:
+                    simple = False
+                    break
+                edges.add(e)
+            if not simple:
+                break
+        if simple:
+            break
+    else:
+        raise RuntimeError("could not draw a simple random regular graph")
+    e = np.array(sorted(edges), np.int64)
+    r = np.concatenate([e[:, 0], e[:, 1]])
+    c = np.concatenate([e[:, 1], e[:, 0]])
+    u = torch.rand(r.size, generator=gen).numpy().astype(np.float32)  # G[r, c]
+    # column sums of G in ascending-row order (fp32)
+    order = np.lexsort((r, c))
+    colsum = np.zeros(n, np.float32)
+    for idx in order:
+        colsum[c[idx]] = np.float32(colsum[c[idx]] + u[idx])
+    wval = (u / colsum[c]).astype(np.float32)
+    # W = G^T: W[c, r] = G[r, c] / colsum[c]; rows of W are columns of G
+    key = np.lexsort((r, c))  # sort by W row (= c), then W col (= r)
+    rows_w, cols_w, vals_w = c[key], r[key], wval[key]
+    rowptr = np.zeros(n + 1, np.int64)
+    np.cumsum(np.bincount(rows_w, minlength=n), out=rowptr[1:])
+    keep = vals_w > 0
+    if not keep.all():  # the >0 selection rule of Neighbors
+        return csr_from_dense(CSR(n, n, rowptr.astype(np.int32), cols_w.astype(np.int32),
+                                  vals_w).dense())
+    return CSR(n, n, rowptr.astype(np.int32), cols_w.astype(np.int32), vals_w)
+
+
+class MixingPlan:
+    """Device form of one W: CSR tensors plus the ring specialisation if it applies."""
+
+    def __init__(self, csr: CSR, device, allow_ring: bool = True):
+        self.csr = csr
+        self.device = torch.device(device)
+        self.n_rows = csr.n_rows
+        self.rowptr = torch.from_numpy(csr.rowptr).to(self.device)
+        self.col = torch.from_numpy(csr.col).to(self.device)
+        self.val = torch.from_numpy(csr.val).to(self.device)
+        ring = csr.ring_weights() if allow_ring else None
+        self.kind = "ring" if ring is not None else "csr"
+        if ring is not None:
+            self.w_prev = torch.from_numpy(ring[0]).to(self.device)
+            self.w_next = torch.from_numpy(ring[1]).to(self.device)
+
+    @classmethod
+    def from_graph(cls, W: Graph, device, allow_ring: bool = True) -> "MixingPlan":
+        return cls(csr_from_dense(W), device, allow_ring)
+
+    def apply(self, X: torch.Tensor, Y: torch.Tensor, P: Optional[int] = None) -> torch.Tensor:
+        from . import ops
+        if self.kind == "ring":
+            return ops.mix_ring(X, Y, self.w_prev, self.w_next, P=P, n_rows=self.n_rows)
+        return ops.mix_csr(X, Y, self.rowptr, self.col, self.val, P=P)
+
+
+def plans_for(graphs: Sequence[Graph], device, allow_ring: bool = True) -> List[MixingPlan]:
+    return [MixingPlan.from_graph(g, device, allow_ring) for g in graphs]

@@ -1,0 +1,211 @@
+"""Tensor-level wrappers over the C-ABI (include/dol_hip.h).
+
+Every function takes CUDA(HIP) fp32 tensors, validates shapes/strides on the
+host (the kernels trust their arguments), and enqueues on the current torch
+stream.  There is deliberately no CPU path: a CPU tensor raises.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import _native
+from ._native import DolNativeError
+
+__all__ = [
+    "DolNativeError", "mix_csr", "mix_ring", "prox_admm_sgd", "admm_dual", "ordered_mean",
+    "ordered_sum", "stream_copy", "dual_workspace_bytes",
+]
+
+
+def _stream(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _check_rows(name: str, t: torch.Tensor, P: Optional[int] = None) -> int:
+    """Validate a stacked [rows, >=P] fp32 device matrix; return its ld."""
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name}: expected a torch.Tensor")
+    if t.device.type != "cuda":
+        raise DolNativeError(f"{name}: tensor is on {t.device}; the HIP engine has no CPU path")
+    if t.dtype != torch.float32:
+        raise TypeError(f"{name}: expected float32, got {t.dtype}")
+    if t.dim() != 2:
+        raise ValueError(f"{name}: expected a 2-D [rows, P] tensor, got shape {tuple(t.shape)}")
+    if t.shape[1] > 1 and t.stride(1) != 1:
+        raise ValueError(f"{name}: rows must be contiguous (stride(1) == 1)")
+    ld = t.stride(0) if t.shape[0] > 1 else max(t.shape[1], 1)
+    if P is not None and t.shape[1] < P:
+        raise ValueError(f"{name}: has {t.shape[1]} columns < P={P}")
+    return int(ld)
+
+
+def _check_vec(name: str, t: Optional[torch.Tensor], P: int, device) -> None:
+    if t is None:
+        return
+    if t.device != device:
+        raise DolNativeError(f"{name}: on {t.device}, expected {device}")
+    if t.dtype != torch.float32 or t.dim() != 1 or t.shape[0] < P or (t.shape[0] > 1 and t.stride(0) != 1):
+        raise ValueError(f"{name}: expected a contiguous float32 vector of >= {P} elements")
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def mix_csr(X: torch.Tensor, Y: torch.Tensor, rowptr: torch.Tensor, col: torch.Tensor,
+            val: torch.Tensor, P: Optional[int] = None) -> torch.Tensor:
+    """Y[i] = sum_e val[e] * X[col[e]] (ascending e, +0 start, no FMA).
+
+    Reference: DIST/simulators.py:91-97 + DIST/clients.py:61-69."""
+    P = X.shape[1] if P is None else P
+    ldx = _check_rows("X", X, P)
+    ldy = _check_rows("Y", Y, P)
+    n = rowptr.shape[0] - 1
+    if Y.shape[0] < n:
+        raise ValueError(f"Y has {Y.shape[0]} rows < {n}")
+    for nm, t, dt in (("rowptr", rowptr, torch.int32), ("col", col, torch.int32), ("val", val, torch.float32)):
+        if t.device != X.device or t.dtype != dt or not t.is_contiguous():
+            raise ValueError(f"{nm}: expected contiguous {dt} on {X.device}")
+    if col.numel() != val.numel():
+        raise ValueError("col and val lengths differ")
+    if X.data_ptr() == Y.data_ptr():
+        raise ValueError("X and Y alias: the Jacobi mix needs two buffers")
+    _native.call("dol_mix_csr_f32", X.data_ptr(), ldx, X.shape[0], Y.data_ptr(), ldy, n, P,
+                 rowptr.data_ptr(), col.data_ptr() if col.numel() else None,
+                 val.data_ptr() if val.numel() else None, _stream(X))
+    return Y
+
+
+def mix_ring(X: torch.Tensor, Y: torch.Tensor, w_prev: torch.Tensor, w_next: torch.Tensor,
+             halo_prev: Optional[torch.Tensor] = None, halo_next: Optional[torch.Tensor] = None,
+             P: Optional[int] = None, n_rows: Optional[int] = None) -> torch.Tensor:
+    """Ring (circle topology) mix; halos are the rows before/after the local block."""
+    P = X.shape[1] if P is None else P
+    n = X.shape[0] if n_rows is None else n_rows
+    ldx = _check_rows("X", X, P)
+    ldy = _check_rows("Y", Y, P)
+    if X.shape[0] < n or Y.shape[0] < n:
+        raise ValueError("X/Y have fewer rows than n_rows")
+    for nm, t in (("w_prev", w_prev), ("w_next", w_next)):
+        if t.device != X.device or t.dtype != torch.float32 or t.numel() < n or not t.is_contiguous():
+            raise ValueError(f"{nm}: expected contiguous float32 [{n}] on {X.device}")
+    if (halo_prev is None) != (halo_next is None):
+        raise ValueError("pass both halos or neither")
+    if halo_prev is None and n < 3:
+        raise ValueError("a wrap-around ring needs >= 3 rows (use mix_csr)")
+    _check_vec("halo_prev", halo_prev, P, X.device)
+    _check_vec("halo_next", halo_next, P, X.device)
+    if X.data_ptr() == Y.data_ptr():
+        raise ValueError("X and Y alias: the Jacobi mix needs two buffers")
+    _native.call("dol_mix_ring_f32", X.data_ptr(), ldx, Y.data_ptr(), ldy, n, P, _ptr(halo_prev),
+                 _ptr(halo_next), w_prev.data_ptr(), w_next.data_ptr(), _stream(X))
+    return Y
+
+
+def prox_admm_sgd(w: torch.Tensor, g: torch.Tensor, buf: Optional[torch.Tensor] = None,
+                  theta: Optional[torch.Tensor] = None, alpha: Optional[torch.Tensor] = None,
+                  rho: float = 0.0, lr: float = 0.01, momentum: float = 0.0, first_step: bool = False,
+                  write_grad: bool = True, P: Optional[int] = None) -> None:
+    """Fused FedProx/FedADMM gradient term + torch.optim.SGD(momentum) step, in place.
+
+    Reference: DEC/clients.py:101-115, :125-139 and SGD.step (:44)."""
+    P = w.shape[1] if P is None else P
+    n = w.shape[0]
+    ldw = _check_rows("w", w, P)
+    ldg = _check_rows("g", g, P)
+    if g.shape[0] < n:
+        raise ValueError("g has fewer rows than w")
+    ldb = 0
+    if momentum != 0.0:
+        if buf is None:
+            raise ValueError("momentum != 0 needs buf")
+        ldb = _check_rows("buf", buf, P)
+        if buf.shape[0] < n:
+            raise ValueError("buf has fewer rows than w")
+    lda = 0
+    if alpha is not None:
+        if theta is None:
+            raise ValueError("alpha needs theta")
+        lda = _check_rows("alpha", alpha, P)
+        if alpha.shape[0] < n:
+            raise ValueError("alpha has fewer rows than w")
+    _check_vec("theta", theta, P, w.device)
+    _native.call("dol_prox_admm_sgd_f32", w.data_ptr(), ldw, _ptr(buf) if momentum != 0.0 else None, ldb,
+                 g.data_ptr(), ldg, _ptr(theta), _ptr(alpha), lda, float(rho), float(lr), float(momentum),
+                 int(bool(first_step)), int(bool(write_grad)), n, P, _stream(w))
+
+
+def dual_workspace_bytes(n_agents: int, P: int) -> int:
+    return int(_native.lib().dol_admm_dual_workspace_bytes(n_agents, P))
+
+
+def admm_dual(alpha: torch.Tensor, w: torch.Tensor, theta: torch.Tensor, rho: float,
+              resid_sq: Optional[torch.Tensor] = None, work: Optional[torch.Tensor] = None,
+              P: Optional[int] = None) -> None:
+    """alpha += rho*(w - theta) for every row (DEC/clients.py:141-144), in place."""
+    P = alpha.shape[1] if P is None else P
+    n = alpha.shape[0]
+    lda = _check_rows("alpha", alpha, P)
+    ldw = _check_rows("w", w, P)
+    if w.shape[0] < n:
+        raise ValueError("w has fewer rows than alpha")
+    _check_vec("theta", theta, P, alpha.device)
+    if resid_sq is not None:
+        if resid_sq.dtype != torch.float64 or resid_sq.numel() < n or resid_sq.device != alpha.device:
+            raise ValueError("resid_sq: expected float64 [n_agents] on the same device")
+        need = dual_workspace_bytes(n, P)
+        if work is None:
+            work = torch.empty(max(need, 8), dtype=torch.uint8, device=alpha.device)
+        elif work.numel() * work.element_size() < need:
+            raise ValueError(f"work: need {need} bytes")
+    _native.call("dol_admm_dual_f32", alpha.data_ptr(), lda, w.data_ptr(), ldw, theta.data_ptr(), float(rho),
+                 n, P, _ptr(resid_sq), _ptr(work) if resid_sq is not None else None, _stream(alpha))
+
+
+def _check_order(order: torch.Tensor, device, n_rows: int) -> None:
+    if order.device != device or order.dtype != torch.int32 or not order.is_contiguous():
+        raise ValueError("order: expected contiguous int32 on the rows' device")
+
+
+def ordered_mean(W: torch.Tensor, order: torch.Tensor, out: Optional[torch.Tensor] = None,
+                 P: Optional[int] = None) -> torch.Tensor:
+    """theta = (((w[o0] + w[o1]) + ...) / m (DEC/servers.py:42-48)."""
+    P = W.shape[1] if P is None else P
+    ldw = _check_rows("W", W, P)
+    _check_order(order, W.device, W.shape[0])
+    m = order.numel()
+    if m < 1:
+        raise ValueError("ordered_mean needs at least one row (the reference indexes w[0])")
+    if out is None:
+        out = torch.empty(P, dtype=torch.float32, device=W.device)
+    _check_vec("out", out, P, W.device)
+    _native.call("dol_ordered_mean_f32", W.data_ptr(), ldw, order.data_ptr(), m, P, out.data_ptr(), _stream(W))
+    return out
+
+
+def ordered_sum(W: torch.Tensor, order: torch.Tensor, acc_in: Optional[torch.Tensor] = None,
+                out: Optional[torch.Tensor] = None, scale: float = 1.0, P: Optional[int] = None) -> torch.Tensor:
+    P = (W.shape[1] if W is not None else acc_in.shape[0]) if P is None else P
+    device = W.device if W is not None else acc_in.device
+    ldw = _check_rows("W", W, P) if W is not None else P
+    m = 0 if order is None else order.numel()
+    if m:
+        _check_order(order, device, W.shape[0])
+    _check_vec("acc_in", acc_in, P, device)
+    if out is None:
+        out = torch.empty(P, dtype=torch.float32, device=device)
+    _check_vec("out", out, P, device)
+    _native.call("dol_ordered_sum_f32", _ptr(W) if m else None, ldw, _ptr(order) if m else None, m, P,
+                 _ptr(acc_in), out.data_ptr(), float(scale), torch.cuda.current_stream(device).cuda_stream)
+    return out
+
+
+def stream_copy(src: torch.Tensor, dst: torch.Tensor) -> torch.Tensor:
+    if src.device.type != "cuda" or dst.device != src.device:
+        raise DolNativeError("stream_copy: device tensors required")
+    if not (src.is_contiguous() and dst.is_contiguous()) or src.numel() != dst.numel():
+        raise ValueError("stream_copy: contiguous tensors of equal size required")
+    _native.call("dol_stream_copy_f32", src.data_ptr(), dst.data_ptr(), src.numel(), _stream(src))
+    return dst

@@ -1,0 +1,180 @@
+"""Agent sharding across ranks (one process per GPU, torch.distributed).
+
+The reference runs every agent in one process and "sends" a row by reading
+another agent's state_dict (DIST/simulators.py:96); its server "all-reduce"
+is a Python loop (DEC/servers.py:44-47).  Here agents are split into
+contiguous blocks, one block per rank:
+
+* ring mixing: the only cross-rank data are the two boundary rows.  Each round
+  the interior rows are mixed on the compute stream while the halo rows travel
+  (send/recv over RCCL/xGMI, or gloo on CPU), then the two boundary rows are
+  mixed.  Results are bit-identical to the single-GPU mix for every world size
+  (each output row sees the same two products added in the same order).
+* global mean (FedAvg / FedProx / FedADMM server average): each rank sums its
+  local sampled rows in sampled order, then `all_reduce(SUM)` and a division
+  by m ("fast", association order differs from the reference by rank), or an
+  ordered chain over ranks in the global sampled order ("exact": bit-identical
+  to DEC/servers.py:42-48, one hop per change of owner).
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+
+from . import ops
+
+
+def shard_bounds(n: int, world: int, rank: int) -> Tuple[int, int]:
+    """Contiguous block [lo, hi) of agent rows owned by `rank`."""
+    base, extra = divmod(n, world)
+    lo = rank * base + min(rank, extra)
+    hi = lo + base + (1 if rank < extra else 0)
+    return lo, hi
+
+
+class ShardedRing:
+    """Ring (circle) mixing of a globally N-agent system, sharded by rows.
+
+    x/y: local [n_local, ld] buffers (allocated here); w_prev/w_next: the
+    GLOBAL ring weights [N] (host or device); the local slice is kept.
+    """
+
+    def __init__(self, n_agents: int, P: int, w_prev, w_next, device, ld: Optional[int] = None,
+                 group=None, alloc: bool = True, mix_ring=None):
+        # mix_ring: kernel entry (defaults to the HIP op); tests inject a CPU checker
+        self._mix = mix_ring if mix_ring is not None else ops.mix_ring
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        if n_agents < max(3, 2 * self.world):
+            raise ValueError("ring sharding needs >= 3 agents and >= 2 agents per rank")
+        self.N, self.P = n_agents, P
+        self.device = torch.device(device)
+        self.lo, self.hi = shard_bounds(n_agents, self.world, self.rank)
+        self.n_local = self.hi - self.lo
+        self.ld = ld if ld is not None else (P + 63) // 64 * 64
+        wp = torch.as_tensor(w_prev, dtype=torch.float32)
+        wn = torch.as_tensor(w_next, dtype=torch.float32)
+        self.w_prev = wp[self.lo:self.hi].contiguous().to(self.device)
+        self.w_next = wn[self.lo:self.hi].contiguous().to(self.device)
+        self.prev_rank = (self.rank - 1) % self.world
+        self.next_rank = (self.rank + 1) % self.world
+        if alloc:
+            self.x = torch.empty(self.n_local, self.ld, dtype=torch.float32, device=self.device)
+            self.y = torch.empty_like(self.x)
+        self.halo_prev = torch.empty(self.ld, dtype=torch.float32, device=self.device)
+        self.halo_next = torch.empty(self.ld, dtype=torch.float32, device=self.device)
+        # optional (start, end) timing events recorded around the interior kernel
+        self.kernel_events = None
+
+    def _exchange(self, x: torch.Tensor):
+        """Post the halo send/recv pairs; returns the requests.
+
+        Order is fixed so that world == 2 (prev == next) still pairs correctly:
+        first the 'downstream' message (my last row -> next rank's halo_prev),
+        then the 'upstream' one (my first row -> prev rank's halo_next)."""
+        P = self.P
+        first, last = x[0, :P], x[self.n_local - 1, :P]
+        ops_ = [
+            dist.P2POp(dist.isend, last, self.next_rank, self.group, tag=0),
+            dist.P2POp(dist.irecv, self.halo_prev[:P], self.prev_rank, self.group, tag=0),
+            dist.P2POp(dist.isend, first, self.prev_rank, self.group, tag=1),
+            dist.P2POp(dist.irecv, self.halo_next[:P], self.next_rank, self.group, tag=1),
+        ]
+        return dist.batch_isend_irecv(ops_)
+
+    def step(self, x: Optional[torch.Tensor] = None, y: Optional[torch.Tensor] = None) -> None:
+        """One Jacobi round Y = W X on the local block (then swap if using own buffers)."""
+        own = x is None
+        x = self.x if own else x
+        y = self.y if own else y
+        n, P = self.n_local, self.P
+        if self.world == 1:
+            self._mix(x, y, self.w_prev, self.w_next, P=P, n_rows=n)
+        else:
+            reqs = self._exchange(x)
+            # interior rows 1..n-2: their neighbours are all local
+            if n > 2:
+                ev = self.kernel_events
+                if ev:
+                    ev[0].record()
+                self._mix(x[1:], y[1:], self.w_prev[1:], self.w_next[1:], halo_prev=x[0],
+                          halo_next=x[n - 1], P=P, n_rows=n - 2)
+                if ev:
+                    ev[1].record()
+            for r in reqs:
+                r.wait()
+            # boundary rows 0 and n-1
+            self._mix(x[0:1], y[0:1], self.w_prev[0:1], self.w_next[0:1], halo_prev=self.halo_prev,
+                      halo_next=x[1], P=P, n_rows=1)
+            self._mix(x[n - 1:n], y[n - 1:n], self.w_prev[n - 1:n], self.w_next[n - 1:n],
+                      halo_prev=x[n - 2], halo_next=self.halo_next, P=P, n_rows=1)
+        if own:
+            self.x, self.y = self.y, self.x
+
+
+def global_mean(local_rows: torch.Tensor, local_order: Sequence[int], m_total: int, P: int,
+                group=None, out: Optional[torch.Tensor] = None, ordered_sum=None) -> torch.Tensor:
+    """'fast' global mean: local ordered partial sum, all_reduce(SUM), / m."""
+    ordered_sum = ordered_sum if ordered_sum is not None else ops.ordered_sum
+    device = local_rows.device
+    if out is None:
+        out = torch.empty(P, dtype=torch.float32, device=device)
+    if len(local_order):
+        idx = torch.as_tensor(list(local_order), dtype=torch.int32, device=device)
+        ordered_sum(local_rows, idx, out=out, P=P)
+    else:
+        out.zero_()
+    if dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(out, op=dist.ReduceOp.SUM, group=group)
+    zero = torch.empty(0, dtype=torch.int32, device=device)
+    return ordered_sum(None, zero, acc_in=out, out=out, scale=float(m_total), P=P)
+
+
+def global_mean_exact(local_rows: torch.Tensor, lo: int, hi: int, order: Sequence[int], P: int,
+                      group=None, out: Optional[torch.Tensor] = None, ordered_sum=None) -> torch.Tensor:
+    """Bit-exact DEC/servers.py:42-48 order across ranks: the running sum hops
+    to the owner of each run of consecutive sampled agents, then is broadcast
+    from the last owner.  `order` holds GLOBAL agent ids; rows [lo, hi) local."""
+    ordered_sum = ordered_sum if ordered_sum is not None else ops.ordered_sum
+    device = local_rows.device
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    m = len(order)
+    if m < 1:
+        raise ValueError("need at least one sampled agent")
+    bounds = [(lo, hi)] if world == 1 else _all_bounds(lo, hi, device, group)
+    owner = [next(r for r, (a, b) in enumerate(bounds) if a <= g < b) for g in order]
+    runs: List[Tuple[int, List[int]]] = []
+    for g, o in zip(order, owner):
+        if runs and runs[-1][0] == o:
+            runs[-1][1].append(g)
+        else:
+            runs.append((o, [g]))
+    acc = out if out is not None else torch.empty(P, dtype=torch.float32, device=device)
+    have = False
+    for k, (o, ids) in enumerate(runs):
+        if o == rank:
+            if k > 0 and runs[k - 1][0] != rank:
+                dist.recv(acc[:P], src=runs[k - 1][0], group=group)
+                have = True
+            idx = torch.as_tensor([g - lo for g in ids], dtype=torch.int32, device=device)
+            last = k == len(runs) - 1
+            ordered_sum(local_rows, idx, acc_in=acc if have else None, out=acc,
+                            scale=float(m) if last else 1.0, P=P)
+            have = True
+            if not last and runs[k + 1][0] != rank:
+                dist.send(acc[:P], dst=runs[k + 1][0], group=group)
+    if world > 1:
+        dist.broadcast(acc[:P], src=runs[-1][0], group=group)
+    return acc
+
+
+def _all_bounds(lo: int, hi: int, device, group=None) -> List[Tuple[int, int]]:
+    world = dist.get_world_size(group)
+    mine = torch.tensor([lo, hi], dtype=torch.int64, device=device)
+    allb = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(allb, mine, group=group)
+    return [(int(t[0]), int(t[1])) for t in allb]

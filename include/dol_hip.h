@@ -1,0 +1,140 @@
+/*
+ * dol_hip.h — C-ABI of the MI355X (gfx950) consensus / primal-dual engine.
+ *
+ * Every entry point replaces one per-agent Python loop of the reference
+ * (AlirezaMoseni/Distributed-Optimization-and-Learning); the reference symbol
+ * each one stands in for is cited on its declaration.  Path shorthand:
+ *   DIST/ = "Distributed Optimization/src/"   (gossip, "Weighted Average")
+ *   DEC/  = "Decentralized Optimization/src/" (FedAvg/FedProx/FedADMM server)
+ *
+ * Conventions (all entry points):
+ *   - Stacked state: agent k's flattened parameter vector is row k of a
+ *     row-major fp32 matrix with leading dimension `ld*` (elements, >= P).
+ *     Flattening order = the model's state_dict() key order.
+ *   - All pointers are caller-owned DEVICE memory (hipMalloc / torch CUDA
+ *     tensors) unless stated; nothing here allocates, frees or synchronises,
+ *     so every call may be captured into a hipGraph.
+ *   - Work is enqueued on the caller's stream `s` (NULL = legacy default).
+ *   - Return 0 on success; DOL_EINVAL (-1) for a bad argument; otherwise
+ *     -(hipError_t) of the failing launch.  dol_last_error() returns a
+ *     thread-local message describing the last failure on this thread.
+ *   - Arithmetic is fp32 with the reference's rounding sequence (documented
+ *     per call); the library is compiled with -ffp-contract=off and uses an
+ *     explicit fused multiply-add only where the reference's CPU path does.
+ */
+#ifndef DOL_HIP_H_
+#define DOL_HIP_H_
+
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DOL_OK 0
+#define DOL_EINVAL (-1)
+
+/* Library version, e.g. 100 for 0.1.0. */
+int dol_version(void);
+
+/* Thread-local description of the last error on this thread ("" if none). */
+const char* dol_last_error(void);
+
+/*
+ * Generic sparse gossip mix  Y[i,:] = sum_{e in rowptr[i]..rowptr[i+1]} val[e] * X[col[e],:]
+ *
+ * Replaces Simulator.Neighbors + Client.consensus + the Jacobi write-back:
+ *   DIST/simulators.py:91-97  (Neighbors: j ascending, keep W[i][j] > 0)
+ *   DIST/clients.py:61-69     (consensus: w_avg = 0; w_avg += x_j * a_ij)
+ *   DIST/simulators.py:148-152 (all rows mixed from the old X, then loaded)
+ * Rounding: acc = +0.0f; for e ascending: acc = fl(acc + fl(val[e]*x)).
+ * The caller builds the CSR with the reference's selection rule (ascending
+ * column, entries with W_ij <= 0 or NaN dropped); an empty row yields zeros.
+ * X and Y must not alias.  col[] indexes rows of X (0 <= col < x_rows).
+ */
+int dol_mix_csr_f32(const float* X, int64_t ldx, int32_t x_rows,
+                    float* Y, int64_t ldy, int32_t n_rows, int64_t P,
+                    const int32_t* rowptr, const int32_t* col, const float* val,
+                    hipStream_t s);
+
+/*
+ * Ring (circle topology) specialisation of dol_mix_csr_f32:
+ *   Y[i,:] = fl(fl(+0 + fl(w_prev[i]*X[i-1,:])) + fl(w_next[i]*X[i+1,:]))
+ * Replaces the same reference code as dol_mix_csr_f32 for
+ * communication_graph("circle", ...) (DIST/simulators.py:42-47), where every
+ * row has exactly the two neighbours i-1 and i+1 (mod n) with W > 0.  Two
+ * addends commute exactly, so this equals the ascending-column order.
+ * Row -1 is `halo_prev` and row n_rows is `halo_next` (each a P-vector);
+ * pass NULL for both to wrap around inside X (single-shard ring, n_rows>=3).
+ * w_prev/w_next: device arrays [n_rows].  X and Y must not alias.
+ */
+int dol_mix_ring_f32(const float* X, int64_t ldx, float* Y, int64_t ldy,
+                     int32_t n_rows, int64_t P,
+                     const float* halo_prev, const float* halo_next,
+                     const float* w_prev, const float* w_next,
+                     hipStream_t s);
+
+/*
+ * Fused local step of n_agents agents (rows of w/buf/g), replacing:
+ *   FedProx_Client.update_model  DEC/clients.py:101-115  g' = fl(g + fl(rho*fl(w-theta)))
+ *   FedAdmm_Client.update_model  DEC/clients.py:125-139  g' = fl(g + fl(alpha + fl(rho*fl(w-theta))))
+ *   FedAvg / gossip local step   DEC/clients.py:85-95, DIST/clients.py:43-49  g' = g
+ * followed by torch.optim.SGD(lr, momentum).step()  (DIST/clients.py:17,49; DEC/clients.py:14,44):
+ *   momentum != 0: buf = first_step ? g' : fl(fl(buf*momentum) + g');  d = buf
+ *   momentum == 0: d = g'
+ *   w = fma(-lr, d, w)            (ATen's vectorised add_(d, alpha=-lr))
+ * theta: [P] (shared by all agents) or NULL (no proximal/ADMM term).
+ * alpha: stacked duals (lda) or NULL (FedProx when theta != NULL).
+ * write_grad != 0 stores g' back into g (the reference mutates param.grad).
+ * buf may be NULL only when momentum == 0.
+ */
+int dol_prox_admm_sgd_f32(float* w, int64_t ldw, float* buf, int64_t ldb,
+                          float* g, int64_t ldg,
+                          const float* theta, const float* alpha, int64_t lda,
+                          float rho, float lr, float momentum,
+                          int first_step, int write_grad,
+                          int32_t n_agents, int64_t P, hipStream_t s);
+
+/*
+ * ADMM dual ascent for n_agents agents, replacing
+ *   FedAdmm_Client.update_duals  DEC/clients.py:141-144 (called at :52)
+ *   alpha = fl(alpha + fl(rho * fl(w - theta)))       (theta: [P], pre-round)
+ * resid_sq (nullable, [n_agents] fp64): receives ||w_k - theta||^2 summed in
+ * a fixed order (deterministic).  It needs `work` (nullable iff resid_sq is
+ * NULL) of dol_admm_dual_workspace_bytes(n_agents, P) bytes.
+ */
+int dol_admm_dual_f32(float* alpha, int64_t lda, const float* w, int64_t ldw,
+                      const float* theta, float rho,
+                      int32_t n_agents, int64_t P,
+                      double* resid_sq, void* work, hipStream_t s);
+int64_t dol_admm_dual_workspace_bytes(int32_t n_agents, int64_t P);
+
+/*
+ * Ordered uniform average, replacing Server.average_weights
+ *   DEC/servers.py:42-48:  acc = w[order[0]]; acc = fl(acc + w[order[k]]) k=1..m-1;
+ *                          theta = fl(acc / (float)m)
+ * order: device int32 [m] of row indices into W (the sampled-client order of
+ * DEC/servers.py:57).  theta: [P], must not alias W.
+ */
+int dol_ordered_mean_f32(const float* W, int64_t ldw, const int32_t* order,
+                         int32_t m, int64_t P, float* theta, hipStream_t s);
+
+/*
+ * Ordered partial sum without the division (building block for the
+ * multi-GPU chain reduce):  acc_out = fl(...fl(acc_in + w[order[0]]) ...)
+ * acc_in NULL: start from w[order[0]] exactly (as DEC/servers.py:43).
+ * acc_out may alias acc_in.  scale != 1 divides the final result:
+ * acc_out = fl(acc / scale) when scale != 1.0f.
+ */
+int dol_ordered_sum_f32(const float* W, int64_t ldw, const int32_t* order,
+                        int32_t m, int64_t P, const float* acc_in,
+                        float* acc_out, float scale, hipStream_t s);
+
+/* Streaming copy dst = src (n floats): HBM calibration kernel for roofline. */
+int dol_stream_copy_f32(const float* src, float* dst, int64_t n, hipStream_t s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DOL_HIP_H_ */

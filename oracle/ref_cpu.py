@@ -1,0 +1,60 @@
+"""Reference-structured CPU consensus round — TEST/BENCH INFRASTRUCTURE.
+
+bench.py's cpu_baseline leg times this on the GPU box's host cores.  It keeps
+the reference's structure and torch CPU ops exactly:
+  * Neighbors (DIST/simulators.py:91-97): scan j = 0..N-1 of W[i] (0-d tensor
+    indexing), keep (W[i][j], agent j's state dict) when W[i][j] > 0;
+  * consensus (DIST/clients.py:61-69): zeros_like + torch.mul(x_j, a) += ...;
+  * synchronous write-back (DIST/simulators.py:151-152): load_state_dict,
+    i.e. an in-place copy into each agent's tensors after all rows are mixed.
+Agents here hold one flat tensor each (the synthetic workload has a single
+parameter block of P floats).
+"""
+from __future__ import annotations
+
+import time
+from typing import Dict, List, Tuple
+
+import torch
+
+
+class Agent:
+    def __init__(self, state: Dict[str, torch.Tensor]):
+        self.state = state
+
+
+def neighbors(i: int, W: torch.Tensor, agents: List[Agent]) -> List[Tuple[torch.Tensor, Dict[str, torch.Tensor]]]:
+    out = []
+    for j in range(len(agents)):
+        a = W[i][j]
+        if a > 0:
+            out.append((a, agents[j].state))
+    return out
+
+
+def consensus(own: Dict[str, torch.Tensor], Ni) -> Dict[str, torch.Tensor]:
+    acc = {k: torch.zeros_like(v) for k, v in own.items()}
+    for a, sd in Ni:
+        for k in sd:
+            acc[k] += torch.mul(sd[k], a)
+    return acc
+
+
+def mixing_round(W: torch.Tensor, agents: List[Agent]) -> None:
+    new = [consensus(ag.state, neighbors(i, W, agents)) for i, ag in enumerate(agents)]
+    for ag, nw in zip(agents, new):
+        for k, v in nw.items():
+            ag.state[k].copy_(v)
+
+
+def time_rounds(W: torch.Tensor, X: torch.Tensor, min_seconds: float = 10.0, max_rounds: int = 50):
+    """Run rounds on agents whose parameters are rows of X until min_seconds
+    have elapsed (at least 2 rounds).  Returns (rounds, seconds)."""
+    agents = [Agent({"w": X[i]}) for i in range(X.shape[0])]
+    mixing_round(W, agents)  # warm-up (allocator, thread pool)
+    t0 = time.perf_counter()
+    r = 0
+    while r < 2 or (time.perf_counter() - t0 < min_seconds and r < max_rounds):
+        mixing_round(W, agents)
+        r += 1
+    return r, time.perf_counter() - t0

@@ -1,0 +1,276 @@
+"""HIP kernels (through the C-ABI) vs the oracle and the reference's golden
+vectors.  Mixing, dual update, ordered mean and the fused local step are
+bit-exact (fp32, same rounding sequence as the reference's torch CPU path);
+the only tolerance is on the fp64 residual norm (a diagnostic whose
+reduction order differs): rtol 1e-12."""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from oracle import bits_equal
+from conftest import golden
+from dolhip import graph as G
+from dolhip import ops
+
+pytestmark = pytest.mark.gpu
+
+
+def dev(a, gpu, dtype=torch.float32):
+    return torch.as_tensor(np.ascontiguousarray(a)).to(device=gpu, dtype=dtype)
+
+
+def padded(a, gpu, extra):
+    """Device copy with leading dimension P + extra (extra=1 forces the scalar path)."""
+    n, P = a.shape
+    t = torch.full((n, P + extra), float("nan"), dtype=torch.float32, device=gpu)
+    t[:, :P] = dev(a, gpu)
+    return t
+
+
+def _mix_cases():
+    return sorted(k[:-3] for k in golden("mix").files if k.endswith("__X"))
+
+
+@pytest.mark.parametrize("extra", [0, 1, 60])
+@pytest.mark.parametrize("case", _mix_cases())
+def test_mix_csr_golden(case, extra, gpu):
+    mix, csr = golden("mix"), golden("csr")
+    gkey, _l, t = case.split("__")
+    c = f"{gkey}__{t}"
+    X = mix[case + "__X"]
+    n, P = X.shape
+    Xd = padded(X, gpu, extra)
+    Yd = padded(np.zeros_like(X), gpu, extra)
+    ops.mix_csr(Xd, Yd, dev(csr[c + "__rowptr"], gpu, torch.int32), dev(csr[c + "__col"], gpu, torch.int32),
+                dev(csr[c + "__val"], gpu), P=P)
+    torch.cuda.synchronize()
+    assert bits_equal(Yd[:, :P].cpu().numpy(), mix[case + "__Y"])
+
+
+@pytest.mark.parametrize("extra", [0, 1])
+@pytest.mark.parametrize("case", _mix_cases())
+def test_mix_ring_golden(case, extra, gpu):
+    mix, csr = golden("mix"), golden("csr")
+    gkey, _l, t = case.split("__")
+    c = f"{gkey}__{t}"
+    n = len(csr[c + "__rowptr"]) - 1
+    rw = G.CSR(n, n, csr[c + "__rowptr"], csr[c + "__col"], csr[c + "__val"]).ring_weights()
+    if rw is None:
+        pytest.skip("not a ring")
+    X = mix[case + "__X"]
+    P = X.shape[1]
+    Xd, Yd = padded(X, gpu, extra), padded(np.zeros_like(X), gpu, extra)
+    ops.mix_ring(Xd, Yd, dev(rw[0], gpu), dev(rw[1], gpu), P=P)
+    torch.cuda.synchronize()
+    assert bits_equal(Yd[:, :P].cpu().numpy(), mix[case + "__Y"])
+
+
+@pytest.mark.parametrize("n,P", [(3, 5), (4, 1027), (5, 4096), (64, (1 << 16) + 3), (257, 12289), (1000, 1024)])
+def test_mix_ring_random_vs_oracle(n, P, gpu):
+    rng = np.random.default_rng(n * 7 + P)
+    X = rng.standard_normal((n, P)).astype(np.float32)
+    wp, wn = rng.random(n).astype(np.float32), rng.random(n).astype(np.float32)
+    Xd, Yd = dev(X, gpu), torch.empty(n, P, device=gpu)
+    ops.mix_ring(Xd, Yd, dev(wp, gpu), dev(wn, gpu))
+    torch.cuda.synchronize()
+    assert bits_equal(Yd.cpu().numpy(), oracle.mix_ring(X, wp, wn))
+
+
+def test_mix_ring_halos_and_subblocks(gpu):
+    """The halo form used by the sharded ring equals the wrap form."""
+    rng = np.random.default_rng(3)
+    n, P = 37, 5003
+    X = rng.standard_normal((n, P)).astype(np.float32)
+    wp, wn = rng.random(n).astype(np.float32), rng.random(n).astype(np.float32)
+    want = oracle.mix_ring(X, wp, wn)
+    Xd, Yd = dev(X, gpu), torch.zeros(n, P, device=gpu)
+    wpd, wnd = dev(wp, gpu), dev(wn, gpu)
+    ops.mix_ring(Xd[1:], Yd[1:], wpd[1:], wnd[1:], halo_prev=Xd[0], halo_next=Xd[n - 1], n_rows=n - 2)
+    ops.mix_ring(Xd[0:1], Yd[0:1], wpd[0:1], wnd[0:1], halo_prev=Xd[n - 1].clone(), halo_next=Xd[1], n_rows=1)
+    ops.mix_ring(Xd[n - 1:], Yd[n - 1:], wpd[n - 1:], wnd[n - 1:], halo_prev=Xd[n - 2], halo_next=Xd[0].clone(),
+                 n_rows=1)
+    torch.cuda.synchronize()
+    assert bits_equal(Yd.cpu().numpy(), want)
+
+
+def test_mix_signed_zero_and_nonfinite(gpu):
+    n, P = 8, 4100
+    X = np.full((n, P), -0.0, np.float32)
+    X[3, 10] = np.inf
+    X[5, 11] = np.nan
+    wp = np.full(n, 0.25, np.float32)
+    wn = np.full(n, 0.75, np.float32)
+    Yd = torch.empty(n, P, device=gpu)
+    ops.mix_ring(dev(X, gpu), Yd, dev(wp, gpu), dev(wn, gpu))
+    Y = Yd.cpu().numpy()
+    want = oracle.mix_ring(X, wp, wn)
+    assert bits_equal(Y, want)
+    assert Y[0, 0].view(np.uint32) == 0  # (+0 + -0) + -0 == +0, as torch.zeros_like + ...
+
+
+@pytest.mark.parametrize("n,deg,P", [(64, 4, 4099), (300, 4, 1024), (50, 12, 777)])
+def test_mix_csr_random_regular_vs_oracle(n, deg, P, gpu):
+    c = G.random_regular_csr(n, deg, seed=n)
+    rng = np.random.default_rng(1)
+    X = rng.standard_normal((n, P)).astype(np.float32)
+    plan = G.MixingPlan(c, gpu)
+    assert plan.kind == "csr"
+    Yd = torch.empty(n, P, device=gpu)
+    plan.apply(dev(X, gpu), Yd)
+    torch.cuda.synchronize()
+    assert bits_equal(Yd.cpu().numpy(), oracle.mix_csr(X, c.rowptr, c.col, c.val))
+
+
+def test_multi_round_mix_plan_and_bank(gpu):
+    from dolhip.bank import AgentBank
+    torch.manual_seed(2028)
+    W = G.communication_graph("circle", "stochastic", 16)[0]
+    plan = G.MixingPlan.from_graph(W, gpu)
+    assert plan.kind == "ring"
+    rng = np.random.default_rng(4)
+    X = rng.standard_normal((16, 999)).astype(np.float32)
+    bank = AgentBank(16, 999, gpu)
+    bank.rows()[:] = dev(X, gpu)
+    bank.mix(plan, steps=5)
+    c = plan.csr
+    want = X
+    for _ in range(5):
+        want = oracle.mix_csr(want, c.rowptr, c.col, c.val)
+    assert bits_equal(bank.rows().cpu().numpy(), want)
+
+
+def _local_keys():
+    L = golden("local_steps")
+    return sorted({k.rsplit("__", 1)[0] for k in L.files})
+
+
+@pytest.mark.parametrize("key", _local_keys())
+def test_fused_local_step_golden(key, gpu):
+    L = golden("local_steps")
+    rho, lr, mom = (float(v) for v in L[key + "__params"])
+    cls = key.split("__")[0]
+    th = None if cls == "FedAvg_Client" else dev(L[key + "__theta"], gpu)
+    al = dev(L[key + "__alpha"][None], gpu) if cls == "FedAdmm_Client" else None
+    for t in range(L[key + "__w"].shape[0]):
+        w = dev(L[key + "__w"][t][None], gpu)
+        b = dev(L[key + "__buf"][t][None], gpu)
+        g = dev(L[key + "__g"][t][None], gpu)
+        ops.prox_admm_sgd(w, g, buf=b, theta=th, alpha=al, rho=rho, lr=lr, momentum=mom, first_step=(t == 0))
+        torch.cuda.synchronize()
+        assert bits_equal(g.cpu().numpy()[0], L[key + "__gp"][t])
+        assert bits_equal(w.cpu().numpy()[0], L[key + "__w1"][t])
+        if mom != 0:
+            assert bits_equal(b.cpu().numpy()[0], L[key + "__buf1"][t])
+
+
+@pytest.mark.parametrize("variant", ["avg", "prox", "admm"])
+@pytest.mark.parametrize("mom,first", [(0.0, False), (0.5, True), (0.5, False), (0.9, False)])
+@pytest.mark.parametrize("extra", [0, 1])
+def test_fused_local_step_random_vs_oracle(variant, mom, first, extra, gpu):
+    rng = np.random.default_rng(9)
+    n, P = 5, 20000 + 3
+    w, g, b = (rng.standard_normal((n, P)).astype(np.float32) for _ in range(3))
+    th = rng.standard_normal(P).astype(np.float32) if variant != "avg" else None
+    al = rng.standard_normal((n, P)).astype(np.float32) if variant == "admm" else None
+    wd, gd, bd = padded(w, gpu, extra), padded(g, gpu, extra), padded(b, gpu, extra)
+    ald = padded(al, gpu, extra) if al is not None else None
+    ops.prox_admm_sgd(wd, gd, buf=bd, theta=None if th is None else dev(th, gpu), alpha=ald, rho=0.1, lr=0.05,
+                      momentum=mom, first_step=first, P=P)
+    torch.cuda.synchronize()
+    w1, b1, g1 = oracle.prox_admm_sgd(w, b, g, th, al, 0.1, 0.05, mom, first)
+    assert bits_equal(wd[:, :P].cpu().numpy(), w1)
+    assert bits_equal(gd[:, :P].cpu().numpy(), g1)
+    if mom != 0:
+        assert bits_equal(bd[:, :P].cpu().numpy(), b1)
+
+
+@pytest.mark.parametrize("rho", ["0.1", "0.01", "1.0"])
+def test_dual_golden(rho, gpu):
+    D = golden("duals")
+    k = f"rho{rho}"
+    a = dev(D[k + "__alpha"], gpu)
+    r = torch.zeros(a.shape[0], dtype=torch.float64, device=gpu)
+    ops.admm_dual(a, dev(D[k + "__w"], gpu), dev(D[k + "__theta"], gpu), float(D[k + "__rho"][0]), resid_sq=r)
+    torch.cuda.synchronize()
+    assert bits_equal(a.cpu().numpy(), D[k + "__alpha1"])
+
+
+@pytest.mark.parametrize("n,P,extra", [(3, 5, 0), (7, 4096 * 3 + 2, 0), (4, 100003, 1), (2, (1 << 20) + 1, 0)])
+def test_dual_random_with_residual(n, P, extra, gpu):
+    rng = np.random.default_rng(P)
+    a, w = (rng.standard_normal((n, P)).astype(np.float32) for _ in range(2))
+    th = rng.standard_normal(P).astype(np.float32)
+    ad = padded(a, gpu, extra)
+    r = torch.zeros(n, dtype=torch.float64, device=gpu)
+    ops.admm_dual(ad, padded(w, gpu, extra), dev(th, gpu), 0.1, resid_sq=r, P=P)
+    torch.cuda.synchronize()
+    a1, r1 = oracle.admm_dual(a, w, th, 0.1)
+    assert bits_equal(ad[:, :P].cpu().numpy(), a1)
+    np.testing.assert_allclose(r.cpu().numpy(), r1, rtol=1e-12)
+
+
+@pytest.mark.parametrize("name", ["m7_mini", "m1_mini", "m10_flat1031", "m3_flat4097"])
+def test_ordered_mean_golden(name, gpu):
+    A = golden("average")
+    W = A[name + "__W"]
+    order = torch.arange(W.shape[0], dtype=torch.int32, device=gpu)
+    th = ops.ordered_mean(dev(W, gpu), order)
+    torch.cuda.synchronize()
+    assert bits_equal(th.cpu().numpy(), A[name + "__theta"])
+
+
+@pytest.mark.parametrize("N,m,P", [(100, 10, 1663370), (64, 64, 4097), (2000, 17, 3)])
+def test_ordered_mean_sampled_order_vs_oracle(N, m, P, gpu):
+    rng = np.random.default_rng(m)
+    W = rng.standard_normal((N, P)).astype(np.float32)
+    order = rng.choice(N, m, replace=False).astype(np.int32)
+    th = ops.ordered_mean(dev(W, gpu), dev(order, gpu, torch.int32))
+    torch.cuda.synchronize()
+    assert bits_equal(th.cpu().numpy(), oracle.ordered_mean(W, order))
+
+
+def test_stream_copy(gpu):
+    x = torch.randn(1 << 20 | 3, device=gpu)
+    y = torch.empty_like(x)
+    ops.stream_copy(x, y)
+    assert torch.equal(x, y)
+
+
+def test_errors_surface_as_exceptions(gpu):
+    x = torch.zeros(4, 8, device=gpu)
+    with pytest.raises(ValueError):
+        ops.mix_ring(x, x, torch.ones(4, device=gpu), torch.ones(4, device=gpu))
+    with pytest.raises(ValueError):
+        ops.ordered_mean(x, torch.zeros(0, dtype=torch.int32, device=gpu))
+
+
+def test_full_size_ring_sampled_rows(gpu):
+    """BASELINE size (8192 agents x 2^20 params, 2 x 32 GiB): every output row
+    depends on two input rows, so sampled rows are checked bit-exactly against
+    the oracle, and a global checksum against an independent fp64 restatement."""
+    N, P = 8192, 1 << 20
+    torch.manual_seed(2028)
+    W = G.communication_graph("circle", "stochastic", N)[0]
+    plan = G.MixingPlan.from_graph(W, gpu)
+    assert plan.kind == "ring"
+    g = torch.Generator(device=gpu).manual_seed(1)
+    X = torch.randn(N, P, device=gpu, generator=g)
+    Y = torch.empty_like(X)
+    plan.apply(X, Y)
+    torch.cuda.synchronize()
+    wp, wn = plan.csr.ring_weights()
+    for i in [0, 1, 2, 4095, 4096, N - 2, N - 1] + list(np.random.default_rng(0).integers(0, N, 8)):
+        i = int(i)
+        rows = X[[(i - 1) % N, (i + 1) % N]].cpu().numpy()
+        want = oracle.mix_ring(np.stack([rows[0], np.zeros(P, np.float32), rows[1]]),
+                               np.array([0, wp[i], 0], np.float32), np.array([0, wn[i], 0], np.float32))[1]
+        assert bits_equal(Y[i].cpu().numpy(), want), i
+    # column sums: sum_i y_i = sum_j (W^T 1)_j x_j, checked in fp64 on 64 columns
+    cols = torch.arange(0, P, P // 64, device=gpu)
+    colw = torch.from_numpy(plan.csr.dense().sum(0).astype(np.float64)).to(gpu)
+    lhs = Y[:, cols].double().sum(0)
+    rhs = (colw[:, None] * X[:, cols].double()).sum(0)
+    torch.testing.assert_close(lhs, rhs, rtol=1e-5, atol=1e-3)
+    del X, Y
+    torch.cuda.empty_cache()
