@@ -109,11 +109,15 @@ __device__ __forceinline__ void stv(V* p, V v) {
 }
 
 // ----------------------------------------------------------------------------
-// Ring mix: one workgroup = one column tile (256 lanes x V) x R consecutive
-// agent rows.  The three-point stencil along the agent axis is carried in a
-// register window, so each X row segment is read once per workgroup and each
-// Y row segment written once: (R+2)/R reads, 1 write.  PF rows are loaded
-// one iteration ahead so every lane keeps PF loads in flight.
+// Ring mix: one workgroup = one column tile (256 lanes x V = 4 KiB of a row)
+// x R consecutive agent rows.  The three-point stencil along the agent axis is
+// carried in a register window; PF rows are loaded one iteration ahead.
+// Measured on MI355X (tools/membench*.hip, 8192 x 2^20): short-lived tiles win
+// — R = 4 with all R+2 loads issued up front (PF >= R), plain loads and
+// nontemporal stores reach 6.14 TB/s against a 6.26 TB/s flat-copy ceiling,
+// while R = 64 long-lived tiles stay near 5.1-5.4.  The halo rows (2 per
+// tile) are re-read from L2: vertically adjacent tiles are n_col_tiles
+// blocks apart (a multiple of 8 -> same XCD) and co-resident.
 // ----------------------------------------------------------------------------
 template <typename V, int PF, bool NT_LOAD, bool NT_STORE>
 __global__ __launch_bounds__(kThreads) void ring_mix_kernel(
@@ -121,10 +125,13 @@ __global__ __launch_bounds__(kThreads) void ring_mix_kernel(
     int n_rows, int64_t c_off, int64_t ncols_v, int64_t n_col_tiles, int rows_per_block,
     const float* __restrict__ halo_prev, const float* __restrict__ halo_next,
     const float* __restrict__ wprev, const float* __restrict__ wnext) {
-  const int64_t b = blockIdx.x;
-  const int64_t ct = b % n_col_tiles;
-  const int rg = static_cast<int>(b / n_col_tiles);
-  const int64_t c = ct * kThreads + threadIdx.x;  // column in units of V
+  // 32-bit block decomposition (grids are < 2^24 blocks); column tile fastest,
+  // so co-resident workgroups share rows and the halo re-reads hit L2
+  const uint32_t b = blockIdx.x;
+  const uint32_t nct = static_cast<uint32_t>(n_col_tiles);
+  const uint32_t ct = b % nct;
+  const int rg = static_cast<int>(b / nct);
+  const int64_t c = int64_t(ct) * kThreads + threadIdx.x;  // column in units of V
   if (c >= ncols_v) return;
   const int r0 = rg * rows_per_block;
   const int r1 = min(r0 + rows_per_block, n_rows);
@@ -444,10 +451,8 @@ void launch_ring_variant(int pf, int nt, const float* X, int64_t ldx, float* Y, 
 int ring_rows_per_block(int n_rows, int64_t n_col_tiles, int pf) {
   int r = env_int("DOL_RING_ROWS", 0);
   if (r > 0) return r;
-  r = 64;
-  // keep >= ~8 workgroups per CU (256 CUs) for small agent counts
-  while (r > pf && n_col_tiles * cdiv(n_rows, r) < 2048) r /= 2;
-  return r < 1 ? 1 : r;
+  (void)n_col_tiles;
+  return pf < 4 ? pf : 4;  // see the ring kernel comment: 4 rows per tile, all loads up front
 }
 
 template <typename V, int RPB>

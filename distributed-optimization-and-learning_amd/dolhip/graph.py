@@ -171,30 +171,40 @@ def csr_from_dense(W: Graph) -> CSR:
 
 
 def random_regular_csr(n: int, degree: int = 4, seed: int = 2028) -> CSR:
-    """Seeded simple random d-regular graph (union of d/2 random Hamiltonian
-    cycles, resampled until simple) with the reference's 'stochastic' weight
-    rule: G = R o A, columns normalised, W = G^T.  Not in the reference; the
-    synthetic mixing workload of BASELINE config 3."""
+    """Seeded simple random d-regular graph with the reference's 'stochastic'
+    weight rule (G = R o A, columns normalised, W = G^T).  Construction: the
+    circulant C_n(1..d/2) under a random relabelling, then n*d degree-
+    preserving double-edge swaps (rejecting self-loops and multi-edges).
+    Not in the reference: the synthetic mixing workload of BASELINE config 3."""
     if degree % 2 or degree < 2 or n <= degree:
         raise ValueError("need an even degree 2 <= d < n")
     gen = torch.Generator().manual_seed(seed)
-    for _ in range(1000):
-        edges = set()
-        simple = True
-        for _k in range(degree // 2):
-            perm = torch.randperm(n, generator=gen).numpy()
-            for a, b in zip(perm, np.roll(perm, -1)):
-                e = (min(a, b), max(a, b))
-                if e in edges:
-                    simple = False
-                    break
-                edges.add(e)
-            if not simple:
-                break
-        if simple:
-            break
-    else:
-        raise RuntimeError("could not draw a simple random regular graph")
+    perm = torch.randperm(n, generator=gen).numpy()
+    elist = []
+    for k in range(1, degree // 2 + 1):
+        for i in range(n):
+            a, b = int(perm[i]), int(perm[(i + k) % n])
+            elist.append((min(a, b), max(a, b)))
+    edges = set(elist)
+    if len(edges) != len(elist):
+        raise RuntimeError("circulant seed graph is not simple")
+    picks = torch.randint(0, len(elist), (2 * n * degree, 2), generator=gen).numpy()
+    flips = torch.randint(0, 2, (n * degree,), generator=gen).numpy()
+    for s_ in range(n * degree):
+        i, j = picks[s_]
+        if i == j:
+            continue
+        (a, b), (c, d) = elist[i], elist[j]
+        if flips[s_]:
+            c, d = d, c
+        e1, e2 = (min(a, d), max(a, d)), (min(c, b), max(c, b))
+        if a == d or c == b or e1 in edges or e2 in edges:
+            continue
+        edges.discard(elist[i])
+        edges.discard(elist[j])
+        edges.add(e1)
+        edges.add(e2)
+        elist[i], elist[j] = e1, e2
     e = np.array(sorted(edges), np.int64)
     r = np.concatenate([e[:, 0], e[:, 1]])
     c = np.concatenate([e[:, 1], e[:, 0]])

@@ -24,6 +24,7 @@ import torch
 import torch.distributed as dist
 
 from . import ops
+from .bank import row_stride
 
 
 def shard_bounds(n: int, world: int, rank: int) -> Tuple[int, int]:
@@ -54,7 +55,7 @@ class ShardedRing:
         self.device = torch.device(device)
         self.lo, self.hi = shard_bounds(n_agents, self.world, self.rank)
         self.n_local = self.hi - self.lo
-        self.ld = ld if ld is not None else (P + 63) // 64 * 64
+        self.ld = ld if ld is not None else row_stride(P)
         wp = torch.as_tensor(w_prev, dtype=torch.float32)
         wn = torch.as_tensor(w_next, dtype=torch.float32)
         self.w_prev = wp[self.lo:self.hi].contiguous().to(self.device)
