@@ -387,13 +387,25 @@ __global__ __launch_bounds__(kThreads) void ordered_sum_kernel(
   *(reinterpret_cast<V*>(out + c_off) + c) = acc;
 }
 
-template <typename V>
-__global__ __launch_bounds__(kThreads) void copy_kernel(const V* __restrict__ src, V* __restrict__ dst,
+// Calibration copy: each block streams one contiguous 16 KiB chunk (4 x f4
+// per lane, nontemporal both ways) and exits — 6.26 TB/s on MI355X, the
+// measured ceiling the mixing kernels are compared with (tools/membench.hip).
+__global__ __launch_bounds__(kThreads) void copy_kernel(const f4* __restrict__ src, f4* __restrict__ dst,
                                                         int64_t n) {
+  const int64_t base = int64_t(blockIdx.x) * kThreads * 4 + threadIdx.x;
+  f4 v[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+    if (base + u * kThreads < n) v[u] = __builtin_nontemporal_load(src + base + u * kThreads);
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+    if (base + u * kThreads < n) __builtin_nontemporal_store(v[u], dst + base + u * kThreads);
+}
+
+__global__ __launch_bounds__(kThreads) void copy_scalar_kernel(const float* __restrict__ src,
+                                                               float* __restrict__ dst, int64_t n) {
   const int64_t stride = int64_t(gridDim.x) * kThreads;
-  for (int64_t i = int64_t(blockIdx.x) * kThreads + threadIdx.x; i < n; i += stride) {
-    __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
-  }
+  for (int64_t i = int64_t(blockIdx.x) * kThreads + threadIdx.x; i < n; i += stride) dst[i] = src[i];
 }
 
 // ----------------------------------------------------------------------------
@@ -661,16 +673,18 @@ int dol_stream_copy_f32(const float* src, float* dst, int64_t n, hipStream_t s) 
   if (n < 0) return fail(DOL_EINVAL, "dol_stream_copy_f32: negative size");
   if (n == 0) { g_err[0] = '\0'; return DOL_OK; }
   if (!src || !dst) return fail(DOL_EINVAL, "dol_stream_copy_f32: null pointer");
-  const int64_t grid = 256 * 8;
   if (aligned16(src) && aligned16(dst)) {
     const int64_t n4 = n / 4;
-    if (n4 > 0)
-      hipLaunchKernelGGL(copy_kernel<f4>, dim3(grid), dim3(kThreads), 0, s, reinterpret_cast<const f4*>(src),
-                         reinterpret_cast<f4*>(dst), n4);
+    if (n4 > 0) {
+      const int64_t grid = cdiv(n4, int64_t(kThreads) * 4);
+      if (grid > kMaxBlocks * 8) return fail(DOL_EINVAL, "dol_stream_copy_f32: too large");
+      hipLaunchKernelGGL(copy_kernel, dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, s,
+                         reinterpret_cast<const f4*>(src), reinterpret_cast<f4*>(dst), n4);
+    }
     if (n % 4)
-      hipLaunchKernelGGL(copy_kernel<float>, dim3(1), dim3(kThreads), 0, s, src + 4 * n4, dst + 4 * n4, n % 4);
+      hipLaunchKernelGGL(copy_scalar_kernel, dim3(1), dim3(kThreads), 0, s, src + 4 * n4, dst + 4 * n4, n % 4);
   } else {
-    hipLaunchKernelGGL(copy_kernel<float>, dim3(grid), dim3(kThreads), 0, s, src, dst, n);
+    hipLaunchKernelGGL(copy_scalar_kernel, dim3(2048), dim3(kThreads), 0, s, src, dst, n);
   }
   return check_launch("dol_stream_copy_f32");
 }
