@@ -257,6 +257,24 @@ __global__ __launch_bounds__(kThreads) void prox_sgd_kernel(
   if constexpr (MODE != 0) *(reinterpret_cast<V*>(B + agent * ldb + c_off) + c) = bf;
 }
 
+// Gradient term alone: g += rho*(w - theta) (+ alpha), w untouched.
+template <typename V, bool ALPHA>
+__global__ __launch_bounds__(kThreads) void prox_grad_kernel(
+    float* __restrict__ G, int64_t ldg, const float* __restrict__ W, int64_t ldw,
+    const float* __restrict__ theta, const float* __restrict__ A, int64_t lda, float rho,
+    int64_t c_off, int64_t ncols_v, int64_t n_col_tiles) {
+  const int64_t blk = blockIdx.x;
+  const int64_t agent = blk / n_col_tiles;
+  const int64_t c = (blk % n_col_tiles) * kThreads + threadIdx.x;
+  if (c >= ncols_v) return;
+  V* gp = reinterpret_cast<V*>(G + agent * ldg + c_off) + c;
+  const V w = *(reinterpret_cast<const V*>(W + agent * ldw + c_off) + c);
+  const V th = *(reinterpret_cast<const V*>(theta + c_off) + c);
+  V t = rho * (w - th);
+  if constexpr (ALPHA) t = *(reinterpret_cast<const V*>(A + agent * lda + c_off) + c) + t;
+  *gp = *gp + t;
+}
+
 // ----------------------------------------------------------------------------
 // ADMM dual update alpha += rho*(w - theta), with optional per-agent
 // ||w-theta||^2 partials (fp64, fixed reduction tree -> deterministic).
@@ -605,6 +623,29 @@ int dol_prox_admm_sgd_f32(float* w, int64_t ldw, float* buf, int64_t ldb, float*
     dispatch_prox<float>(th, al, mode, wg, w, ldw, buf, ldb, g, ldg, theta, alpha, lda, rho, lr,
                          momentum, n_agents, cs.n4 * 4, cs.tail, s);
   return check_launch("dol_prox_admm_sgd_f32");
+}
+
+int dol_prox_grad_f32(float* g, int64_t ldg, const float* w, int64_t ldw, const float* theta,
+                      const float* alpha, int64_t lda, float rho, int32_t n_agents, int64_t P,
+                      hipStream_t s) {
+  if (n_agents < 0 || P < 0) return fail(DOL_EINVAL, "dol_prox_grad_f32: negative size");
+  if (n_agents == 0 || P == 0) { g_err[0] = '\0'; return DOL_OK; }
+  if (!g || !w || !theta) return fail(DOL_EINVAL, "dol_prox_grad_f32: null pointer");
+  if (ldg < P || ldw < P || (alpha && lda < P)) return fail(DOL_EINVAL, "dol_prox_grad_f32: ld < P");
+  const bool vec_ok = row_vec_ok(g, ldg) && row_vec_ok(w, ldw) && row_vec_ok(theta, 0) &&
+                      row_vec_ok(alpha, alpha ? lda : 0);
+  const ColSplit cs = split_cols(P, vec_ok);
+  auto launch = [&](auto vtag, int64_t c_off, int64_t nc) {
+    using V = decltype(vtag);
+    const int64_t nct = cdiv(nc, kThreads);
+    const dim3 grid(static_cast<unsigned>(nct * n_agents));
+    if (alpha) hipLaunchKernelGGL((prox_grad_kernel<V, true>), grid, dim3(kThreads), 0, s, g, ldg, w, ldw, theta, alpha, lda, rho, c_off, nc, nct);
+    else hipLaunchKernelGGL((prox_grad_kernel<V, false>), grid, dim3(kThreads), 0, s, g, ldg, w, ldw, theta, alpha, lda, rho, c_off, nc, nct);
+  };
+  if (cdiv(cs.n4 + cs.tail, kThreads) * n_agents > kMaxBlocks) return fail(DOL_EINVAL, "dol_prox_grad_f32: too large");
+  if (cs.n4 > 0) launch(f4{}, 0, cs.n4);
+  if (cs.tail > 0) launch(float{}, cs.n4 * 4, cs.tail);
+  return check_launch("dol_prox_grad_f32");
 }
 
 int64_t dol_admm_dual_workspace_bytes(int32_t n_agents, int64_t P) {

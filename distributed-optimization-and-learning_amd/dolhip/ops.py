@@ -15,7 +15,7 @@ from ._native import DolNativeError
 
 __all__ = [
     "DolNativeError", "mix_csr", "mix_ring", "prox_admm_sgd", "admm_dual", "ordered_mean",
-    "ordered_sum", "stream_copy", "dual_workspace_bytes",
+    "ordered_sum", "stream_copy", "dual_workspace_bytes", "prox_grad",
 ]
 
 
@@ -135,6 +135,26 @@ def prox_admm_sgd(w: torch.Tensor, g: torch.Tensor, buf: Optional[torch.Tensor] 
     _native.call("dol_prox_admm_sgd_f32", w.data_ptr(), ldw, _ptr(buf) if momentum != 0.0 else None, ldb,
                  g.data_ptr(), ldg, _ptr(theta), _ptr(alpha), lda, float(rho), float(lr), float(momentum),
                  int(bool(first_step)), int(bool(write_grad)), n, P, _stream(w))
+
+
+def prox_grad(g: torch.Tensor, w: torch.Tensor, theta: torch.Tensor, rho: float,
+              alpha: Optional[torch.Tensor] = None, P: Optional[int] = None) -> None:
+    """g += rho*(w - theta) (+ alpha), in place: the update_model gradient term alone
+    (DEC/clients.py:108-111, :132-135)."""
+    P = g.shape[1] if P is None else P
+    n = g.shape[0]
+    ldg = _check_rows("g", g, P)
+    ldw = _check_rows("w", w, P)
+    if w.shape[0] < n:
+        raise ValueError("w has fewer rows than g")
+    lda = 0
+    if alpha is not None:
+        lda = _check_rows("alpha", alpha, P)
+        if alpha.shape[0] < n:
+            raise ValueError("alpha has fewer rows than g")
+    _check_vec("theta", theta, P, g.device)
+    _native.call("dol_prox_grad_f32", g.data_ptr(), ldg, w.data_ptr(), ldw, theta.data_ptr(), _ptr(alpha), lda,
+                 float(rho), n, P, _stream(g))
 
 
 def dual_workspace_bytes(n_agents: int, P: int) -> int:

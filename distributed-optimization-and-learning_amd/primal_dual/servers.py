@@ -1,0 +1,150 @@
+"""Federated servers (DEC/servers.py) on the HIP engine.
+
+Same plugin convention as the reference: `Foo_Server` trains `Foo_Client`
+(class looked up by name, DEC/servers.py:22).  The N clients' parameters are
+rows of one AgentBank; the global model is a separate 1-row bank whose row is
+theta.  `average_weights` is the ordered mean kernel over bank rows in the
+sampled order (bit-identical to the reference's sequential sum / m).
+"""
+import copy
+import time
+
+import numpy as np
+import torch
+from tqdm import tqdm
+
+import _engine  # noqa: F401
+from dolhip import ops
+from dolhip.agent import RowState, engine_device
+from dolhip.bank import AgentBank, layout_of
+from dolhip.models import select_model
+from utils import get_dataset, exp_details, setup_seed
+import clients as _clients
+from clients import FedAvg_Client, FedAdmm_Client, FedProx_Client  # noqa: F401
+
+
+def _client_class(server_cls_name: str):
+    name = server_cls_name.replace("_Server", "_Client")
+    cls = getattr(_clients, name, None) or globals().get(name)
+    if cls is None:
+        raise KeyError(name)  # the reference fails the same way (globals()[...])
+    return cls
+
+
+class Server(object):
+    def __init__(self, args):
+        self.args = args
+        self.history = []
+        self.global_round = 0
+        setup_seed(args.seed)
+        model = self.select_global_model(self.args.model, self.args.device)
+        train_dataset, test_dataset, user_groups = get_dataset(args)
+        cls = _client_class(type(self).__name__)
+        self.global_client = cls(args=self.args, train_set=None, test_set=test_dataset,
+                                 idxs=range(len(test_dataset)), model=copy.deepcopy(model))
+        self.clients = []
+        for idx in range(self.args.num_users):
+            self.clients.append(cls(args=self.args, train_set=train_dataset, test_set=None,
+                                    idxs=user_groups[idx], model=copy.deepcopy(model)))
+        self.device = engine_device(args)
+        self.bank = AgentBank(self.args.num_users, layout_of(model), self.device)
+        for i, c in enumerate(self.clients):
+            c.attach(self.bank, i)
+        if args.verbose:
+            exp_details(args)
+            print("random seed =", args.seed)
+            print()
+            print(model)
+
+    def select_global_model(self, model, device):
+        return select_model(model, device if device is not None else "cuda")
+
+    def average_weights(self, w):
+        """Ordered uniform average (DEC/servers.py:42-48): new tensors, sum in
+        list order, true fp32 division by len(w).  Rows of this server's bank
+        are averaged in place of copies; other state dicts are staged."""
+        if len(w) == 0:
+            raise IndexError("list index out of range")  # as w[0] in the reference
+        if all(isinstance(s, RowState) and s.bank is w[0].bank for s in w):
+            bank = w[0].bank
+            out = torch.empty(bank.P, dtype=torch.float32, device=bank.device)
+            bank.ordered_mean([s.row for s in w], out=out)
+            return bank.unflatten(out)
+        keys = list(w[0].keys())
+        ref = w[0]
+        out = {}
+        for k in keys:
+            X = torch.stack([sd[k].reshape(-1) for sd in w]).to(torch.float32)
+            if X.device.type != "cuda":
+                X = X.to(self.device)
+            order = torch.arange(len(w), dtype=torch.int32, device=X.device)
+            out[k] = ops.ordered_mean(X, order).view(ref[k].shape)
+        return out
+
+    def run(self, frac, rounds):
+        start_time = time.time()
+        m = max(int(frac * self.args.num_users), 1)
+        test_acc, test_loss = [], []
+        train_loss = []
+        for _ in tqdm(range(rounds)):
+            print(f"\n | Global Training Round : {self.global_round + 1} |\n")
+            idxs_users = np.random.choice(range(self.args.num_users), m, replace=False)
+            local_weights, local_losses = [], []
+            theta = self.global_client.flat_params()  # read-only for the whole round
+            for i, idx in enumerate(idxs_users):
+                if self.args.verbose:
+                    print(" | #{:2d}: {:2d} |".format(i + 1, idx))
+                lsum, loss = self.clients[idx].update_weights(global_round=self.global_round, theta=theta)
+                local_weights.append(lsum)  # a live bank-row view: stable until the next round
+                local_losses.append(loss)
+            loss_avg = sum(local_losses) / len(local_losses)
+            train_loss.append(loss_avg)
+            mean_acc_all, _ = self.avg_trainig_calculator()
+            self.update_global_model(local_weights)
+            test_acc_1, test_loss_1 = self.global_client.inference("test")
+            test_acc.append(test_acc_1)
+            test_loss.append(test_loss_1)
+            mean_train_loss = np.mean(np.array(train_loss))
+            print("\ntest accuracy:{:.2f}%\n".format(100 * test_acc_1))
+            print(f" \nAvg Training Stats after {self.global_round + 1} global rounds:")
+            print("Training Loss : {:.3f}".format(mean_train_loss))
+            self.history.append({"round": self.global_round, "test_acc": test_acc_1, "test_loss": test_loss_1,
+                                 "train_loss": mean_train_loss, "train_acc": mean_acc_all})
+            self.global_round += 1
+        print("\n Total Run Time: {0:0.4f}".format(time.time() - start_time))
+        print(f" \n Results after {rounds} global rounds of training:")
+        print("|---- Test Accuracy: {:.2f}%".format(100 * test_acc[-1]))
+
+    def tarining(self):
+        pass
+
+    def avg_trainig_calculator(self):
+        """Mean train-split accuracy/loss over ALL clients (DEC/servers.py:85-93)."""
+        avg_acc, avg_loss = 0.0, 0.0
+        self.global_client.model.eval()
+        n = self.args.num_users
+        if self.args.skip_train_eval:
+            return float("nan"), float("nan")
+        for c in range(n):
+            acc, loss = self.clients[c].inference("train")
+            avg_acc += acc / n
+            avg_loss += loss / n
+        return avg_acc, avg_loss
+
+    def update_global_model(self, local_weights):
+        theta = self.average_weights(local_weights)
+        g = self.global_client
+        with torch.no_grad():
+            g.bank.flatten(theta, out=g.flat_params())
+
+
+class FedAdmm_Server(Server):
+    """Averages the plain local weights, as the reference (DEC/servers.py:121-127)."""
+
+
+class FedAvg_Server(Server):
+    """DEC/servers.py:129-135."""
+
+
+class FedProx_Server(Server):
+    """DEC/servers.py:137-143."""

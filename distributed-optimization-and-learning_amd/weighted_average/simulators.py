@@ -1,0 +1,207 @@
+"""Gossip simulators (DIST/simulators.py) on the HIP engine.
+
+Same classes, constructor order (seed -> model -> data -> W -> clients, so the
+global torch/numpy RNG streams are consumed as in the reference) and round
+structure.  The mixing step — per-agent Neighbors scan + consensus +
+load_state_dict (DIST/simulators.py:147-152) — becomes ONE kernel launch
+over the stacked agent rows (AgentBank.mix with the ring or CSR plan of W[t]),
+bit-identical to the reference's arithmetic.
+"""
+import copy
+import time
+
+import torch
+from tqdm import tqdm
+
+import _engine  # noqa: F401
+from dolhip import graph as G
+from dolhip.bank import AgentBank, layout_of
+from dolhip.agent import engine_device
+from dolhip.models import select_model
+from utils import setup_seed, exp_details, get_dataset
+from clients import Client
+
+
+class Simulator(object):
+    def __init__(self, args):
+        self.args = args
+        self.history = []
+        self.global_round = 0
+        setup_seed(args.seed)
+        model = self.select_global_model(self.args.model, self.args.device)
+        train_dataset, test_dataset, user_groups = get_dataset(args)
+        self.clients = []
+        self.adjacent_matrix = self.communication_graph(args.topology, args.mode, args.num_users)
+        for idx in range(self.args.num_users):
+            self.clients.append(Client(args=self.args, train_set=train_dataset, test_set=test_dataset,
+                                       idxs=user_groups[idx], model=copy.deepcopy(model)))
+        # all agents' parameters become rows of one HBM bank
+        self.device = engine_device(args)
+        self.bank = AgentBank(self.args.num_users, layout_of(model), self.device)
+        for i, c in enumerate(self.clients):
+            c.attach(self.bank, i)
+        self._plans = {}
+        if args.verbose:
+            exp_details(args)
+            print("random seed =", args.seed)
+            print()
+            print(model)
+
+    def select_global_model(self, model, device):
+        return select_model(model, device if device is not None else "cuda")
+
+    def communication_graph(self, topology, mode, n):
+        """W[t] exactly as DIST/simulators.py:40-86 (bounded Sinkhorn)."""
+        kw = {}
+        if self.args.sinkhorn_max_iters is not None:
+            kw["sinkhorn_max_iters"] = self.args.sinkhorn_max_iters
+        if self.args.sinkhorn_tol is not None:
+            kw["sinkhorn_tol"] = self.args.sinkhorn_tol
+        return G.communication_graph(topology, mode, n, verbose=bool(self.args.verbose), **kw)
+
+    def plan(self, t: int) -> G.MixingPlan:
+        p = self._plans.get(t)
+        if p is None:
+            p = G.MixingPlan.from_graph(self.adjacent_matrix[t], self.device)
+            self._plans[t] = p
+        return p
+
+    def mix(self, graph_index: int, steps: int = 1) -> None:
+        """X <- W[t] X on every agent at once (synchronous, as :147-152)."""
+        self.bank.mix(self.plan(graph_index), steps=steps)
+
+    def run(self, rounds):
+        pass
+
+    def Neighbors(self, i, graph):
+        """[(W[i][j], state_dict of agent j)] for j ascending with W[i][j] > 0
+        (DIST/simulators.py:91-97), read from the CSR form of the graph."""
+        csr = G.csr_from_dense(graph)
+        s, e = csr.rowptr[i], csr.rowptr[i + 1]
+        return [(graph[i][int(j)], self.clients[int(j)].model.state_dict()) for j in csr.col[s:e]]
+
+    def _print_graph(self, graph):
+        print("\n | Communication Graph")
+        rows = graph.numpy() if isinstance(graph, torch.Tensor) else graph
+        if len(rows) <= 32:
+            for row in rows:
+                print(row)
+        else:
+            print(f"   [{len(rows)} x {len(rows)} mixing matrix]")
+        print()
+
+    def report(self, local_losses, test_loss_1, test_acc_1):
+        loss_avg = sum(local_losses) / len(local_losses)
+        test_loss_avg = sum(test_loss_1) / len(test_loss_1)
+        test_acc_avg = sum(test_acc_1) / len(test_acc_1)
+        print(f" \nAvg Training Stats after {self.global_round + 1} global rounds:")
+        print("Training Loss : {:.3f}".format(loss_avg))
+        print("Test Loss : {:.3f}".format(test_loss_avg))
+        print("Test ACC : {:.2f}".format(test_acc_avg))
+        self.history.append({"round": self.global_round, "avg_test_acc": test_acc_avg,
+                             "avg_test_loss": test_loss_avg, "avg_train_loss": loss_avg})
+        self.global_round += 1
+
+    # shared pieces of the round loops -------------------------------------
+    def _eval_after_mix(self, test_acc_1, test_loss_1, label="Before Local Update"):
+        for client in self.clients:
+            test_acc, test_loss = client.inference("test")
+            client.history[self.global_round] = {"test_hist": {"test_loss": test_loss, "test_acc": test_acc}}
+            test_acc_1.append(test_acc)
+            test_loss_1.append(test_loss)
+            print(f"| {label} | Test Loss : {test_loss:2.3f} | Test ACC: {test_acc:4.3f} |")
+
+    def _local_updates(self, local_losses):
+        for i, client in enumerate(self.clients):
+            if self.args.verbose:
+                print(f" | #{i + 1:2d} |")
+            loss = client.local_update(global_round=self.global_round)
+            local_losses.append(loss)
+            test_acc, test_loss = client.inference("test")
+            print(f"| After  Local Update | Test Loss : {test_loss:2.3f} | Test ACC: {test_acc:4.3f} |")
+
+
+class NoConsDecFedAvg(Simulator):
+    """Local training only, no communication (DIST/simulators.py:110-131)."""
+
+    def run(self, rounds):
+        start_time = time.time()
+        for _ in tqdm(range(rounds)):
+            print(f"\n | Local Training Round : {self.global_round + 1} |\n")
+            local_losses, test_acc_1, test_loss_1 = [], [], []
+            for i, client in enumerate(self.clients):
+                if self.args.verbose:
+                    print(f" | #{i + 1:2d} |")
+                client.history[self.global_round] = {}
+                loss = client.local_update(global_round=self.global_round)
+                local_losses.append(loss)
+                test_acc, test_loss = client.inference("test")
+                test_acc_1.append(test_acc)
+                test_loss_1.append(test_loss)
+                client.history[self.global_round]["test_hist"] = {"test_loss": test_loss, "test_acc": test_acc}
+                print(f"| After  Local Update | Test Loss : {test_loss:2.3f} | Test ACC: {test_acc:4.3f} |")
+            self.report(local_losses, test_loss_1, test_acc_1)
+        print("\n Total Run Time: {0:0.4f}".format(time.time() - start_time))
+
+
+class DecFedAvg(Simulator):
+    """Gossip: mix with W[t], evaluate, local SGD (DIST/simulators.py:133-167)."""
+
+    def run(self, rounds):
+        start_time = time.time()
+        for _ in tqdm(range(rounds)):
+            print(f"\n | Local Training Round : {self.global_round + 1} |\n")
+            local_losses, test_acc_1, test_loss_1 = [], [], []
+            t = self.global_round % len(self.adjacent_matrix)
+            self._print_graph(self.adjacent_matrix[t])
+            self.mix(t)
+            self._eval_after_mix(test_acc_1, test_loss_1)
+            self._local_updates(local_losses)
+            self.report(local_losses, test_loss_1, test_acc_1)
+        print("\n Total Run Time: {0:0.4f}".format(time.time() - start_time))
+
+
+class Centeralized(NoConsDecFedAvg):
+    """One user, one local epoch (DIST/simulators.py:169-174; mutates args like the reference)."""
+
+    def __init__(self, args):
+        args.num_users = 1
+        args.local_ep = 1
+        args.iid = True
+        super().__init__(args)
+
+
+class FedLCon(Simulator):
+    """`eps` consensus steps per round, then local SGD (DIST/simulators.py:176-212).
+
+    By default the eps mixing steps all take effect (X <- W^eps X) and args are
+    used as given — the behaviour the notebook's saved output shows
+    (WA.ipynb cell[36]).  args.reference_compat=True reproduces the shipped
+    code instead: __init__ forces num_users=1, local_ep=1, iid=True, and only
+    the first of the eps steps takes effect (new_weights is never reset)."""
+
+    def __init__(self, args):
+        if args.reference_compat:
+            args.num_users = 1
+            args.local_ep = 1
+            args.iid = True
+        super().__init__(args)
+
+    def run(self, rounds, eps):
+        start_time = time.time()
+        for _ in tqdm(range(rounds)):
+            print(f"\n | Local Training Round : {self.global_round + 1} |\n")
+            local_losses, test_acc_1, test_loss_1 = [], [], []
+            t = self.global_round % len(self.adjacent_matrix)
+            for j in range(eps):
+                print(f"\n| Consesnsus Round {j} |")
+            if eps > 0:
+                self.mix(t, steps=1 if self.args.reference_compat else eps)
+            self._eval_after_mix(test_acc_1, test_loss_1, label="Consensus")
+            self._local_updates(local_losses)
+            self.report(local_losses, test_loss_1, test_acc_1)
+        print("\n Total Run Time: {0:0.4f}".format(time.time() - start_time))
+
+
+class GossipLearning(Simulator):
+    """Empty in the reference (DIST/simulators.py:215-217)."""

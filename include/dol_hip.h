@@ -97,6 +97,18 @@ int dol_prox_admm_sgd_f32(float* w, int64_t ldw, float* buf, int64_t ldb,
                           int32_t n_agents, int64_t P, hipStream_t s);
 
 /*
+ * The proximal / ADMM gradient term alone, in place (no optimizer step):
+ *   FedProx_Client.update_model  DEC/clients.py:108-111  g = fl(g + fl(rho*fl(w-theta)))
+ *   FedAdmm_Client.update_model  DEC/clients.py:132-135  g = fl(g + fl(alpha + fl(rho*fl(w-theta))))
+ * Used when a client's update_model is called on its own (the reference runs
+ * optimizer.step() separately, DEC/clients.py:44); the default local step
+ * fuses both into dol_prox_admm_sgd_f32.  alpha NULL = FedProx.
+ */
+int dol_prox_grad_f32(float* g, int64_t ldg, const float* w, int64_t ldw,
+                      const float* theta, const float* alpha, int64_t lda,
+                      float rho, int32_t n_agents, int64_t P, hipStream_t s);
+
+/*
  * ADMM dual ascent for n_agents agents, replacing
  *   FedAdmm_Client.update_duals  DEC/clients.py:141-144 (called at :52)
  *   alpha = fl(alpha + fl(rho * fl(w - theta)))       (theta: [P], pre-round)

@@ -45,6 +45,8 @@ def lib():
         L.oracle_prox_admm_sgd_f32.argtypes = [_f32p, _i64, _f32p, _i64, _f32p, _i64, _f32p, _f32p, _i64,
                                                ctypes.c_float, ctypes.c_float, ctypes.c_float,
                                                ctypes.c_int, ctypes.c_int, _i32, _i64]
+        L.oracle_prox_grad_f32.argtypes = [_f32p, _i64, _f32p, _i64, _f32p, _f32p, _i64, ctypes.c_float, _i32, _i64]
+        L.oracle_prox_grad_f32.restype = None
         L.oracle_admm_dual_f32.argtypes = [_f32p, _i64, _f32p, _i64, _f32p, ctypes.c_float, _i32, _i64, _f64p]
         L.oracle_ordered_mean_f32.argtypes = [_f32p, _i64, _i32p, _i32, _i64, _f32p]
         L.oracle_ordered_sum_f32.argtypes = [_f32p, _i64, _i32p, _i32, _i64, _f32p, _f32p, ctypes.c_float]
@@ -98,6 +100,15 @@ def prox_admm_sgd(w, buf, g, theta, alpha, rho, lr, momentum, first_step, write_
     lib().oracle_prox_admm_sgd_f32(_p(w), P, _p(buf), P, _p(g), P, _p(th), _p(al), P,
                                    rho, lr, momentum, int(first_step), int(write_grad), n, P)
     return w, buf, g
+
+
+def prox_grad(g, w, theta, alpha, rho):
+    g = _f32c(g).copy()
+    w = _f32c(w)
+    n, P = g.shape
+    al = None if alpha is None else _f32c(alpha)
+    lib().oracle_prox_grad_f32(_p(g), P, _p(w), P, _p(_f32c(theta)), _p(al), P, rho, n, P)
+    return g
 
 
 def admm_dual(alpha, w, theta, rho):

@@ -34,3 +34,21 @@ def gpu():
         pytest.skip("no GPU")
     import torch
     return torch.device("cuda:0")
+
+
+PROJECT_MODULES = ("_engine", "models", "utils", "sampling", "clients", "simulators", "servers")
+
+
+def load_project(name, modules):
+    """Import the flat modules of one drop-in project (weighted_average /
+    primal_dual) the way the reference's notebooks do (their dir on sys.path),
+    purging the other project's same-named modules first."""
+    import importlib
+    for m in PROJECT_MODULES:
+        sys.modules.pop(m, None)
+    path = os.path.join(PKG, name)
+    sys.path.insert(0, path)
+    try:
+        return {m: importlib.import_module(m) for m in modules}
+    finally:
+        sys.path.remove(path)

@@ -284,12 +284,55 @@ def gen_average(dec_srv):
     return out
 
 
+def gen_host(dist_models, dist_sampling, dec_sampling):
+    """Reference model init under a seed (layout + default-init RNG stream) and
+    the user partitions (numpy RNG call sequence) on fixed synthetic labels."""
+    out = {}
+    for name in ("Model1", "Model3"):
+        torch.manual_seed(2028)
+        m = getattr(dist_models, name)()
+        sd = m.state_dict()
+        flat = np.concatenate([v.numpy().reshape(-1) for v in sd.values()])
+        out[f"{name}__keys"] = np.array(list(sd.keys()))
+        out[f"{name}__shapes"] = np.array([str(tuple(v.shape)) for v in sd.values()])
+        out[f"{name}__sample"] = flat[::4999].copy()
+        out[f"{name}__sum"] = np.array([flat.astype(np.float64).sum(), np.abs(flat.astype(np.float64)).sum()])
+        out[f"{name}__P"] = np.array([flat.size])
+    labels = np.random.default_rng(5).integers(0, 10, 1200)
+
+    class _DS:
+        def __init__(self, t):
+            self.targets = torch.from_numpy(t)
+
+        def __len__(self):
+            return len(self.targets)
+
+    ds = _DS(labels)
+    for iid in (True, False):
+        np.random.seed(77)
+        args = _Obj(num_users=6, shards=2)
+        g = dist_sampling.iid_split(ds, args) if iid else dist_sampling.noniid_split(ds, args)
+        for u in range(6):
+            out[f"dist_iid{iid}__u{u}"] = np.array(sorted(float(i) for i in g[u]))
+            if not iid:
+                out[f"dist_iid{iid}__u{u}__order"] = np.asarray(g[u], np.float64)
+        out[f"dist_iid{iid}__after"] = np.random.random(3)
+    np.random.seed(78)
+    g = dec_sampling.mnist_iid(ds, 10)
+    for u in range(10):
+        out[f"dec_iid__u{u}"] = np.array(sorted(int(i) for i in g[u]))
+    out["dec_iid__after"] = np.random.random(3)
+    return out
+
+
 def main():
     _placeholder_torchvision()
-    dist = _import_project(DIST_SRC, ["simulators", "clients"])
+    dist = _import_project(DIST_SRC, ["simulators", "clients", "models", "sampling"])
     graphs, csr = gen_graphs(dist["simulators"])
     mix = gen_mix(dist["simulators"], dist["clients"], graphs)
-    dec = _import_project(DEC_SRC, ["servers", "clients"])
+    dist_models, dist_sampling = dist["models"], dist["sampling"]
+    dec = _import_project(DEC_SRC, ["servers", "clients", "sampling"])
+    host = gen_host(dist_models, dist_sampling, dec["sampling"])
     local = gen_local_steps(dec["clients"])
     duals = gen_duals(dec["clients"])
     avg = gen_average(dec["servers"])
@@ -300,6 +343,7 @@ def main():
     np.savez_compressed(os.path.join(OUT, "local_steps.npz"), **local)
     np.savez_compressed(os.path.join(OUT, "duals.npz"), **duals)
     np.savez_compressed(os.path.join(OUT, "average.npz"), **avg)
+    np.savez_compressed(os.path.join(OUT, "host.npz"), **host)
     with open(os.path.join(OUT, "META.txt"), "w") as f:
         for k, v in meta.items():
             f.write(f"{k}={v}\n")

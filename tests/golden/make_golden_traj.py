@@ -1,0 +1,100 @@
+"""Golden end-to-end trajectories from the REFERENCE (run in the build
+container; needs /root/reference):   python tests/golden/make_golden_traj.py
+
+Runs the shipped DecFedAvg (DIST/simulators.py:133-167) and FedAvg / FedProx /
+FedAdmm servers (DEC/servers.py:50-81) for 2 rounds on CPU, on the seeded
+synthetic MNIST-shaped data of dolhip.data.synthetic_pair (MNIST is not
+available offline).  The reference's get_dataset is replaced by one that
+builds that data and then partitions users with the reference's OWN sampling
+functions, so the numpy RNG is consumed exactly as in its get_dataset.
+Recorded: `history` numbers and, per agent, a strided sample + norms of the
+final flattened parameters.  torchvision: placeholder module only (unused).
+"""
+import contextlib
+import io
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "distributed-optimization-and-learning_amd"))
+sys.path.insert(0, HERE)
+from make_golden import _import_project, _placeholder_torchvision, DIST_SRC, DEC_SRC  # noqa: E402
+from dolhip.data import synthetic_pair  # noqa: E402
+
+STRIDE = 4999
+
+DIST_ARGS = dict(rounds=2, num_users=6, local_ep=1, local_bs=64, lr=0.01, topology="circle", mode="stochastic",
+                 model="Model1", dataset="synthetic", iid=False, shards=2, seed=2028, momentum=0.5,
+                 verbose=False, synthetic_train=1200, synthetic_test=200)
+DEC_ARGS = dict(num_users=10, local_ep=1, local_bs=50, lr=0.1, model="Model1", dataset="synthetic", iid=True,
+                rho=0.1, seed=2022, momentum=0.5, verbose=False, synthetic_train=1000, synthetic_test=200)
+FRAC, ROUNDS = 0.3, 2
+
+
+def flat(sd):
+    return torch.cat([v.detach().reshape(-1).float().cpu() for v in sd.values()]).numpy()
+
+
+def summary(vec):
+    return {"sample": vec[::STRIDE].tolist(), "l2": float(np.linalg.norm(vec.astype(np.float64))),
+            "sum": float(vec.astype(np.float64).sum())}
+
+
+def run_dist():
+    mods = _import_project(DIST_SRC, ["utils", "sampling", "simulators"])
+    U, S, sim = mods["utils"], mods["sampling"], mods["simulators"]
+
+    def get_dataset(args):
+        train, test = synthetic_pair("synthetic", args.synthetic_train, args.synthetic_test, 1234)
+        groups = S.iid_split(train, args) if args.iid else S.noniid_split(train, args)
+        return train, test, groups
+
+    sim.get_dataset = get_dataset
+    args = U.DotDict(dict(DIST_ARGS, device="cpu"))
+    with contextlib.redirect_stdout(io.StringIO()):
+        s = sim.DecFedAvg(args)
+        s.run(args.rounds)
+    return {"history": s.history, "agents": [summary(flat(c.model.state_dict())) for c in s.clients]}
+
+
+def run_dec(server_name):
+    mods = _import_project(DEC_SRC, ["utils", "sampling", "servers"])
+    U, S, srv = mods["utils"], mods["sampling"], mods["servers"]
+
+    def get_dataset(args):
+        train, test = synthetic_pair("synthetic", args.synthetic_train, args.synthetic_test, 1234)
+        groups = S.mnist_iid(train, args.num_users)
+        return train, test, groups
+
+    srv.get_dataset = get_dataset
+    args = U.DotDict(dict(DEC_ARGS, device="cpu"))
+    with contextlib.redirect_stdout(io.StringIO()):
+        s = getattr(srv, server_name)(args)
+        s.run(FRAC, ROUNDS)
+    out = {"history": [{k: float(v) for k, v in h.items()} for h in s.history],
+           "global": summary(flat(s.global_client.model.state_dict())),
+           "clients": [summary(flat(c.model.state_dict())) for c in s.clients]}
+    if server_name == "FedAdmm_Server":
+        out["alpha"] = [summary(flat(c.alpha)) for c in s.clients]
+    return out
+
+
+def main():
+    _placeholder_torchvision()
+    res = {"dist_args": DIST_ARGS, "dec_args": DEC_ARGS, "frac": FRAC, "rounds": ROUNDS, "stride": STRIDE,
+           "torch": torch.__version__, "numpy": np.__version__,
+           "DecFedAvg": run_dist()}
+    for name in ("FedAvg_Server", "FedProx_Server", "FedAdmm_Server"):
+        res[name] = run_dec(name)
+    with open(os.path.join(HERE, "trajectories.json"), "w") as f:
+        json.dump(res, f)
+    print("wrote trajectories.json")
+
+
+if __name__ == "__main__":
+    main()
