@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline (profiling runs)")
     ap.add_argument("--no-copy", action="store_true", help="skip the copy-kernel calibration")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_ring_8192x1M.json"))
+    ap.add_argument("--no-primal-dual", action="store_true", help="skip the secondary primal/dual round")
+    ap.add_argument("--pd-steps", type=int, default=10)
     return ap.parse_args()
 
 
@@ -107,6 +109,74 @@ def cpu_baseline(n_agents: int, P: int, seconds: float, full_agents: int):
                    f"in {sec:.2f} s = {rate:.3f} rounds/s; value = that x {n_agents}/{full_agents} "
                    f"(per-byte extrapolation to {full_agents} agents)"),
     }
+
+
+def primal_dual_round(N: int, P: int, world: int, rank: int, device, steps: int):
+    """Secondary measurement (BASELINE config 4, ADMM side): one FedADMM round
+    over ALL agents = fused ADMM-gradient + momentum-SGD step
+    (dol_prox_admm_sgd_f32, DEC/clients.py:125-139 + SGD.step), dual ascent
+    (dol_admm_dual_f32, :141-144) and the global mean of the new weights
+    (ordered sum of the local rows + all_reduce across ranks + /N,
+    DEC/servers.py:42-48).  Timed like the headline (barrier, max over
+    ranks); each kernel's share from HIP events."""
+    from dolhip import bank as B, ops, parallel
+    lo, hi = parallel.shard_bounds(N, world, rank)
+    n = hi - lo
+    ld = B.row_stride(P)
+    g = torch.Generator(device=device).manual_seed(7 + rank)
+    bufs = {k: torch.empty(n, ld, dtype=torch.float32, device=device) for k in ("w", "g", "mom", "alpha")}
+    for t in bufs.values():
+        t.normal_(generator=g)
+    theta = torch.empty(ld, dtype=torch.float32, device=device).normal_(generator=g)
+    order = torch.arange(n, dtype=torch.int32, device=device)
+    names = ("sgd", "dual", "mean")
+    ev = {k: [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+          for k in names}
+
+    def one(k=None):
+        e = (lambda nm: ev[nm][k]) if k is not None else (lambda nm: None)
+        def rec(nm, i):
+            if e(nm):
+                e(nm)[i].record()
+        rec("sgd", 0)
+        ops.prox_admm_sgd(bufs["w"], bufs["g"], buf=bufs["mom"], theta=theta, alpha=bufs["alpha"], rho=0.1,
+                          lr=0.1, momentum=0.5, first_step=False, write_grad=False, P=P)
+        rec("sgd", 1)
+        rec("dual", 0)
+        ops.admm_dual(bufs["alpha"], bufs["w"], theta, 0.1, P=P)
+        rec("dual", 1)
+        rec("mean", 0)
+        parallel.global_mean(bufs["w"], order, N, P, out=theta)
+        rec("mean", 1)
+
+    one()
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        one(k)
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    el = float(el.item())
+    row_bytes = n * P * 4
+    alg = {"sgd": 6 * row_bytes, "dual": 3 * row_bytes, "mean": row_bytes + P * 4}  # compulsory bytes per launch
+    kern = {}
+    for nm in names:
+        ms = float(np.mean([a.elapsed_time(b) for a, b in ev[nm]]))
+        kern[nm] = {"ms": ms, "GBps": alg[nm] / (ms / 1e3) / 1e9, "frac": alg[nm] / (ms / 1e3) / 1e9 / HBM_PEAK_GBPS,
+                    "algorithmic_bytes": alg[nm]}
+    for t in bufs.values():
+        del t
+    bufs.clear()
+    torch.cuda.empty_cache()
+    return {"rounds_per_s": steps / el, "ms_per_round": el / steps * 1e3, "agents": N, "params": P,
+            "what": "fused ADMM-grad+momentum-SGD step, dual ascent, global mean (all agents)",
+            "kernels": kern}
 
 
 def main():
@@ -167,10 +237,13 @@ def main():
     achieved = alg_bytes / (kern_ms / 1e3) / 1e9
 
     copy_gbps = None
+    del ring.x, ring.y
+    torch.cuda.empty_cache()
     if not args.no_copy:
-        del ring.y
-        torch.cuda.empty_cache()
         copy_gbps = copy_peak(device)
+    pd_round = None
+    if not args.no_primal_dual:
+        pd_round = primal_dual_round(N, P, world, rank, device, args.pd_steps)
 
     traffic = None
     traffic_src = None
@@ -225,6 +298,7 @@ def main():
                 "copy_kernel_GBps": copy_gbps,
             },
             "cpu_baseline": cpu,
+            "primal_dual_round": pd_round,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -124,7 +124,10 @@ def global_mean(local_rows: torch.Tensor, local_order: Sequence[int], m_total: i
     if out is None:
         out = torch.empty(P, dtype=torch.float32, device=device)
     if len(local_order):
-        idx = torch.as_tensor(list(local_order), dtype=torch.int32, device=device)
+        if isinstance(local_order, torch.Tensor) and local_order.device == device:
+            idx = local_order
+        else:
+            idx = torch.as_tensor(list(local_order), dtype=torch.int32, device=device)
         ordered_sum(local_rows, idx, out=out, P=P)
     else:
         out.zero_()
