@@ -426,6 +426,105 @@ __global__ __launch_bounds__(kThreads) void copy_scalar_kernel(const float* __re
   for (int64_t i = int64_t(blockIdx.x) * kThreads + threadIdx.x; i < n; i += stride) dst[i] = src[i];
 }
 
+
+// ----------------------------------------------------------------------------
+// Dense mix Y = W X on fp32 MFMA (v_mfma_f32_32x32x2_f32), for dense W
+// (complete / Erdos-Renyi / time-varying graphs).  Block tile 128 x 128,
+// BK = 32; 4 waves in 2 x 2, each owning a 64 x 64 output sub-tile as 2 x 2
+// MFMA accumulators (64 AGPR/VGPR).  The next K-tile is loaded into registers
+// while the current one feeds the MFMAs (one LDS buffer, two barriers per K
+// tile).  A is stored k-major in LDS so both fragments are 32 consecutive
+// floats per half-wave (conflict-free ds_read_b32).  Numerics: each output is
+// an fma chain over k ascending (exact f32 MFMA), NOT the reference's
+// mul-then-add with W_ij <= 0 skipped — a tolerance path, opt-in.
+// ----------------------------------------------------------------------------
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kDBM = 128, kDBN = 128, kDBK = 32, kDPad = 4;
+
+template <bool VEC_A, bool VEC_B>
+__global__ __launch_bounds__(256, 1) void dense_mix_mfma_kernel(
+    const float* __restrict__ W, int64_t ldw, const float* __restrict__ X, int64_t ldx,
+    float* __restrict__ Y, int64_t ldy, int M, int K, int64_t P, uint32_t n_row_tiles) {
+  __shared__ float As[kDBK][kDBM + kDPad];
+  __shared__ float Bs[kDBK][kDBN + kDPad];
+  const uint32_t b = blockIdx.x;
+  const int m0 = int(b % n_row_tiles) * kDBM;       // row tiles fastest: an X panel is
+  const int64_t n0 = int64_t(b / n_row_tiles) * kDBN;  // reused by consecutive blocks
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  // staging maps: A 128 rows x 32 k (4 f4 per thread), B 32 k x 128 cols (4 f4 per thread)
+  const int ar = t >> 1, ak = (t & 1) * 16;
+  const int bk = t >> 3, bc = (t & 7) * 16;
+  f4 ra[4], rb[4];
+  auto load_tiles = [&](int k0) {
+    const int row = m0 + ar;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = k0 + ak + 4 * j;
+      if constexpr (VEC_A) {
+        ra[j] = (row < M && k < K) ? *reinterpret_cast<const f4*>(W + int64_t(row) * ldw + k) : f4{0.f, 0.f, 0.f, 0.f};
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ra[j][q] = (row < M && k + q < K) ? W[int64_t(row) * ldw + k + q] : 0.f;
+      }
+    }
+    const int kr = k0 + bk;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t c = n0 + bc + 4 * j;
+      if (kr < K && c + 3 < P && VEC_B) {
+        rb[j] = *reinterpret_cast<const f4*>(X + int64_t(kr) * ldx + c);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) rb[j][q] = (kr < K && c + q < P) ? X[int64_t(kr) * ldx + c + q] : 0.f;
+      }
+    }
+  };
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  load_tiles(0);
+  for (int k0 = 0; k0 < K; k0 += kDBK) {
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) As[ak + 4 * j + q][ar] = ra[j][q];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) *reinterpret_cast<f4*>(&Bs[bk][bc + 4 * j]) = rb[j];
+    __syncthreads();
+    if (k0 + kDBK < K) load_tiles(k0 + kDBK);
+    const int kh = lane >> 5, li = lane & 31;
+#pragma unroll
+    for (int kk = 0; kk < kDBK / 2; ++kk) {
+      const int k = 2 * kk + kh;
+      const float a0 = As[k][wm * 64 + li], a1 = As[k][wm * 64 + 32 + li];
+      const float b0 = Bs[k][wn * 64 + li], b1 = Bs[k][wn * 64 + 32 + li];
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+    }
+  }
+  // C/D map (gfx950, dtype-independent): col = lane & 31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int64_t col = n0 + wn * 64 + j * 32 + (lane & 31);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (row < M && col < P) Y[int64_t(row) * ldy + col] = acc[i][j][r];
+      }
+    }
+}
+
 // ----------------------------------------------------------------------------
 // host-side launch helpers
 // ----------------------------------------------------------------------------
@@ -596,6 +695,26 @@ int dol_mix_ring_f32(const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t
                                        w_prev, w_next, s);
   }
   return check_launch("dol_mix_ring_f32");
+}
+
+int dol_mix_dense_f32(const float* W, int64_t ldw, const float* X, int64_t ldx, float* Y, int64_t ldy,
+                      int32_t M, int32_t K, int64_t P, hipStream_t s) {
+  if (M < 0 || K < 0 || P < 0) return fail(DOL_EINVAL, "dol_mix_dense_f32: negative size");
+  if (M == 0 || P == 0) { g_err[0] = '\0'; return DOL_OK; }
+  if (!W || !X || !Y) return fail(DOL_EINVAL, "dol_mix_dense_f32: null pointer");
+  if (ldw < K || ldx < P || ldy < P) return fail(DOL_EINVAL, "dol_mix_dense_f32: ld too small");
+  if (X == Y) return fail(DOL_EINVAL, "dol_mix_dense_f32: X and Y alias");
+  const uint32_t nrt = static_cast<uint32_t>(cdiv(M, kDBM));
+  const int64_t nct = cdiv(P, kDBN);
+  if (int64_t(nrt) * nct > (int64_t(1) << 31)) return fail(DOL_EINVAL, "dol_mix_dense_f32: too large");
+  const bool va = aligned16(W) && ldw % 4 == 0 && K % 4 == 0;
+  const bool vb = aligned16(X) && ldx % 4 == 0;
+  const dim3 grid(static_cast<unsigned>(int64_t(nrt) * nct));
+  if (va && vb) hipLaunchKernelGGL((dense_mix_mfma_kernel<true, true>), grid, dim3(256), 0, s, W, ldw, X, ldx, Y, ldy, M, K, P, nrt);
+  else if (va) hipLaunchKernelGGL((dense_mix_mfma_kernel<true, false>), grid, dim3(256), 0, s, W, ldw, X, ldx, Y, ldy, M, K, P, nrt);
+  else if (vb) hipLaunchKernelGGL((dense_mix_mfma_kernel<false, true>), grid, dim3(256), 0, s, W, ldw, X, ldx, Y, ldy, M, K, P, nrt);
+  else hipLaunchKernelGGL((dense_mix_mfma_kernel<false, false>), grid, dim3(256), 0, s, W, ldw, X, ldx, Y, ldy, M, K, P, nrt);
+  return check_launch("dol_mix_dense_f32");
 }
 
 int dol_prox_admm_sgd_f32(float* w, int64_t ldw, float* buf, int64_t ldb, float* g, int64_t ldg,

@@ -146,9 +146,8 @@ class CSR:
 
     def dense(self) -> np.ndarray:
         d = np.zeros((self.n_rows, self.n_cols), np.float32)
-        for i in range(self.n_rows):
-            s, e = self.rowptr[i], self.rowptr[i + 1]
-            d[i, self.col[s:e]] = self.val[s:e]
+        rows = np.repeat(np.arange(self.n_rows), np.diff(self.rowptr))
+        d[rows, self.col] = self.val
         return d
 
 
@@ -230,27 +229,38 @@ def random_regular_csr(n: int, degree: int = 4, seed: int = 2028) -> CSR:
 class MixingPlan:
     """Device form of one W: CSR tensors plus the ring specialisation if it applies."""
 
-    def __init__(self, csr: CSR, device, allow_ring: bool = True):
+    def __init__(self, csr: CSR, device, allow_ring: bool = True, dense: bool = False):
+        """kind: 'ring' (bit-exact, ring kernel), 'csr' (bit-exact, any W), or
+        'dense' (opt-in: fp32 MFMA GEMM over the dense W, tolerance path)."""
         self.csr = csr
         self.device = torch.device(device)
         self.n_rows = csr.n_rows
         self.rowptr = torch.from_numpy(csr.rowptr).to(self.device)
         self.col = torch.from_numpy(csr.col).to(self.device)
         self.val = torch.from_numpy(csr.val).to(self.device)
-        ring = csr.ring_weights() if allow_ring else None
-        self.kind = "ring" if ring is not None else "csr"
+        ring = csr.ring_weights() if (allow_ring and not dense) else None
+        self.kind = "dense" if dense else ("ring" if ring is not None else "csr")
         if ring is not None:
             self.w_prev = torch.from_numpy(ring[0]).to(self.device)
             self.w_next = torch.from_numpy(ring[1]).to(self.device)
+        if dense:
+            # the CSR's selection (W_ij > 0 kept, NaN/negatives dropped) densified
+            self.W = torch.from_numpy(csr.dense()).to(self.device)
+
+    @property
+    def density(self) -> float:
+        return self.csr.nnz / max(1, self.csr.n_rows * self.csr.n_cols)
 
     @classmethod
-    def from_graph(cls, W: Graph, device, allow_ring: bool = True) -> "MixingPlan":
-        return cls(csr_from_dense(W), device, allow_ring)
+    def from_graph(cls, W: Graph, device, allow_ring: bool = True, dense: bool = False) -> "MixingPlan":
+        return cls(csr_from_dense(W), device, allow_ring, dense)
 
     def apply(self, X: torch.Tensor, Y: torch.Tensor, P: Optional[int] = None) -> torch.Tensor:
         from . import ops
         if self.kind == "ring":
             return ops.mix_ring(X, Y, self.w_prev, self.w_next, P=P, n_rows=self.n_rows)
+        if self.kind == "dense":
+            return ops.mix_dense(self.W, X, Y, P=P)
         return ops.mix_csr(X, Y, self.rowptr, self.col, self.val, P=P)
 
 

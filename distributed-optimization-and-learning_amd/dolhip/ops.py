@@ -14,7 +14,7 @@ from . import _native
 from ._native import DolNativeError
 
 __all__ = [
-    "DolNativeError", "mix_csr", "mix_ring", "prox_admm_sgd", "admm_dual", "ordered_mean",
+    "DolNativeError", "mix_csr", "mix_ring", "mix_dense", "prox_admm_sgd", "admm_dual", "ordered_mean",
     "ordered_sum", "stream_copy", "dual_workspace_bytes", "prox_grad",
 ]
 
@@ -75,6 +75,21 @@ def mix_csr(X: torch.Tensor, Y: torch.Tensor, rowptr: torch.Tensor, col: torch.T
     _native.call("dol_mix_csr_f32", X.data_ptr(), ldx, X.shape[0], Y.data_ptr(), ldy, n, P,
                  rowptr.data_ptr(), col.data_ptr() if col.numel() else None,
                  val.data_ptr() if val.numel() else None, _stream(X))
+    return Y
+
+
+def mix_dense(W: torch.Tensor, X: torch.Tensor, Y: torch.Tensor, P: Optional[int] = None) -> torch.Tensor:
+    """Y = W X on fp32 MFMA (fma chain over k; tolerance path, see dol_hip.h)."""
+    P = X.shape[1] if P is None else P
+    ldw = _check_rows("W", W)
+    ldx = _check_rows("X", X, P)
+    ldy = _check_rows("Y", Y, P)
+    M, K = W.shape
+    if X.shape[0] < K or Y.shape[0] < M:
+        raise ValueError(f"shapes: W {tuple(W.shape)}, X {tuple(X.shape)}, Y {tuple(Y.shape)}")
+    if X.data_ptr() == Y.data_ptr():
+        raise ValueError("X and Y alias")
+    _native.call("dol_mix_dense_f32", W.data_ptr(), ldw, X.data_ptr(), ldx, Y.data_ptr(), ldy, M, K, P, _stream(X))
     return Y
 
 

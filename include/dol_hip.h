@@ -76,6 +76,21 @@ int dol_mix_ring_f32(const float* X, int64_t ldx, float* Y, int64_t ldy,
                      hipStream_t s);
 
 /*
+ * Dense mix on the matrix cores:  Y[M,P] = W[M,K] . X[K,P]   (fp32 MFMA)
+ * For dense mixing matrices (communication_graph("compelete", ...), Erdos-
+ * Renyi, time-varying W; DIST/simulators.py:54-58 and :59-64 with stochastic
+ * weights), replacing the same Neighbors + consensus loop as dol_mix_csr_f32.
+ * Numerics: per output an fma chain over k ascending (v_mfma_f32_32x32x2_f32),
+ * not the reference's separately rounded mul-then-add with W_ij <= 0 skipped:
+ * results differ from the reference by at most ~K ulp-scaled sum|W||X|
+ * (error bound gamma_K); use dol_mix_csr_f32 when bit-exactness is required.
+ * W row-major with ldw >= K; X, Y row stride ldx, ldy >= P; X, Y must not alias.
+ */
+int dol_mix_dense_f32(const float* W, int64_t ldw, const float* X, int64_t ldx,
+                      float* Y, int64_t ldy, int32_t M, int32_t K, int64_t P,
+                      hipStream_t s);
+
+/*
  * Fused local step of n_agents agents (rows of w/buf/g), replacing:
  *   FedProx_Client.update_model  DEC/clients.py:101-115  g' = fl(g + fl(rho*fl(w-theta)))
  *   FedAdmm_Client.update_model  DEC/clients.py:125-139  g' = fl(g + fl(alpha + fl(rho*fl(w-theta))))

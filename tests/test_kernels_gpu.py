@@ -274,3 +274,60 @@ def test_full_size_ring_sampled_rows(gpu):
     torch.testing.assert_close(lhs, rhs, rtol=1e-5, atol=1e-3)
     del X, Y
     torch.cuda.empty_cache()
+
+
+# --------------------------------------------------------------------------- dense (MFMA) mix
+def _gamma_bound(W, X):
+    """Rigorous bound for an fp32 fma chain of length K: |Y - Y64| <= gamma_K * sum|W||X|,
+    gamma_K = K u / (1 - K u), u = 2^-24."""
+    K = W.shape[1]
+    u = 2.0 ** -24
+    return (K * u / (1 - K * u)) * (np.abs(W.astype(np.float64)) @ np.abs(X.astype(np.float64)))
+
+
+@pytest.mark.parametrize("M,K,P", [(256, 256, 1024), (130, 37, 1031), (64, 64, 3)])
+def test_mix_dense_identity_and_permutation_exact(M, K, P, gpu):
+    rng = np.random.default_rng(M + K)
+    X = rng.standard_normal((K, P)).astype(np.float32)
+    for name in ("id", "perm"):
+        W = np.zeros((M, K), np.float32)
+        src = np.arange(M) % K if name == "id" else rng.integers(0, K, M)
+        W[np.arange(M), src] = 1.0
+        Y = torch.empty(M, P, device=gpu)
+        ops.mix_dense(dev(W, gpu), dev(X, gpu), Y)
+        torch.cuda.synchronize()
+        assert bits_equal(Y.cpu().numpy(), X[src]), name  # one nonzero per row: fma chain is exact
+
+
+@pytest.mark.parametrize("n,P", [(16, 4099), (256, 8192), (1000, 513)])
+def test_mix_dense_stochastic_within_gamma_bound(n, P, gpu):
+    torch.manual_seed(2028)
+    Wt = G.communication_graph("compelete", "stochastic", n)[0]
+    plan = G.MixingPlan.from_graph(Wt, gpu, dense=True)
+    assert plan.kind == "dense"
+    rng = np.random.default_rng(n)
+    X = rng.standard_normal((n, P)).astype(np.float32)
+    Y = torch.empty(n, P, device=gpu)
+    plan.apply(dev(X, gpu), Y)
+    torch.cuda.synchronize()
+    Wd = plan.csr.dense()
+    want64 = Wd.astype(np.float64) @ X.astype(np.float64)
+    err = np.abs(Y.cpu().numpy().astype(np.float64) - want64)
+    assert np.all(err <= _gamma_bound(Wd, X) + 1e-30)
+    # and close to the bit-exact CSR path
+    exact = oracle.mix_csr(X, plan.csr.rowptr, plan.csr.col, plan.csr.val)
+    assert np.all(np.abs(Y.cpu().numpy() - exact) <= 2 * _gamma_bound(Wd, X) + 1e-30)
+
+
+@pytest.mark.parametrize("admm", [False, True])
+@pytest.mark.parametrize("extra", [0, 1])
+def test_prox_grad_term_vs_oracle(admm, extra, gpu):
+    rng = np.random.default_rng(21)
+    n, P = 3, 70001
+    g, w = (rng.standard_normal((n, P)).astype(np.float32) for _ in range(2))
+    th = rng.standard_normal(P).astype(np.float32)
+    al = rng.standard_normal((n, P)).astype(np.float32) if admm else None
+    gd = padded(g, gpu, extra)
+    ops.prox_grad(gd, padded(w, gpu, extra), dev(th, gpu), 0.1, alpha=padded(al, gpu, extra) if admm else None, P=P)
+    torch.cuda.synchronize()
+    assert bits_equal(gd[:, :P].cpu().numpy(), oracle.prox_grad(g, w, th, al, 0.1))

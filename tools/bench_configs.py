@@ -1,0 +1,68 @@
+"""Secondary mixing workloads (BASELINE configs 3 and 5): rounds/s and GB/s of
+one X <- W X round for ring / random-regular / (optional) dense W.
+
+  python tools/bench_configs.py [--agents 1024 8192] [--params 1048576] [--reps 10]
+Prints one JSON line per (topology, N).  Algorithmic bytes = 2*N*P*4 (each
+row read once, written once), as in the headline."""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "distributed-optimization-and-learning_amd"))
+
+import torch  # noqa: E402
+
+from dolhip import graph as G  # noqa: E402
+from dolhip.bank import row_stride  # noqa: E402
+
+
+def time_plan(plan, X, Y, P, reps):
+    for _ in range(2):
+        plan.apply(X, Y, P=P)
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        plan.apply(X, Y, P=P)
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--agents", type=int, nargs="+", default=[1024, 8192])
+    ap.add_argument("--params", type=int, default=1 << 20)
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--topologies", nargs="+", default=["ring", "rr4"])
+    a = ap.parse_args()
+    dev = torch.device("cuda")
+    P = a.params
+    for N in a.agents:
+        ld = row_stride(P)
+        X = torch.empty(N, ld, device=dev).normal_()
+        Y = torch.empty_like(X)
+        for topo in a.topologies:
+            t0 = time.time()
+            if topo == "ring":
+                torch.manual_seed(2028)
+                plan = G.MixingPlan.from_graph(G.communication_graph("circle", "stochastic", N)[0], dev)
+            elif topo.startswith("rr"):
+                plan = G.MixingPlan(G.random_regular_csr(N, int(topo[2:]), seed=2028), dev)
+            else:
+                raise SystemExit(f"unknown topology {topo}")
+            build_s = time.time() - t0
+            ms = time_plan(plan, X, Y, P, a.reps)
+            alg = 2 * N * P * 4
+            print(json.dumps({"topology": topo, "kernel": plan.kind, "agents": N, "params": P, "nnz": plan.csr.nnz,
+                              "ms": ms, "rounds_per_s": 1e3 / ms, "GBps": alg / (ms / 1e3) / 1e9,
+                              "frac_of_8TBps": alg / (ms / 1e3) / 1e9 / 8000.0, "plan_build_s": build_s}), flush=True)
+        del X, Y
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
