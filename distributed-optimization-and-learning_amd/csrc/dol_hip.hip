@@ -18,6 +18,7 @@
 #include <string.h>
 #include <stdarg.h>
 #include <algorithm>
+#include <type_traits>
 
 #include "../../include/dol_hip.h"
 
@@ -163,6 +164,49 @@ __global__ __launch_bounds__(kThreads) void ring_mix_kernel(
     q[1] = q[PF + 1];
 #pragma unroll
     for (int k = 0; k < PF; ++k) q[2 + k] = nx[k];
+  }
+}
+
+
+// ----------------------------------------------------------------------------
+// Temporally blocked ring mix: STEPS synchronous rounds in one HBM pass
+// (FedLCon's eps consensus steps, DIST/simulators.py:190-196).  A tile of R
+// output rows loads R + 2*STEPS rows once and applies the 3-point stencil
+// STEPS times in registers; level t is valid on [t, R + 2*STEPS - t).  Every
+// intermediate uses the single-round formula (fl(fl(+0 + wp*a) + wn*b)), so the
+// result is bit-identical to STEPS launches of ring_mix_kernel.  Wrap-around
+// ring inside X (one shard).
+// ----------------------------------------------------------------------------
+template <int STEPS, int R>
+__global__ __launch_bounds__(kThreads) void ring_steps_kernel(
+    const float* __restrict__ X, int64_t ldx, float* __restrict__ Y, int64_t ldy, int n_rows,
+    int64_t ncols_v, uint32_t n_col_tiles, const float* __restrict__ wprev,
+    const float* __restrict__ wnext) {
+  constexpr int L = R + 2 * STEPS;
+  const uint32_t b = blockIdx.x;
+  const uint32_t ct = b % n_col_tiles;
+  const int r0 = static_cast<int>(b / n_col_tiles) * R;
+  const int64_t c = int64_t(ct) * kThreads + threadIdx.x;
+  if (c >= ncols_v) return;
+  auto wrap = [&](int r) { r %= n_rows; return r < 0 ? r + n_rows : r; };
+  f4 v[L];
+#pragma unroll
+  for (int i = 0; i < L; ++i) v[i] = reinterpret_cast<const f4*>(X + int64_t(wrap(r0 - STEPS + i)) * ldx)[c];
+#pragma unroll
+  for (int t = 1; t <= STEPS; ++t) {
+    f4 prev_old = v[t - 1];
+#pragma unroll
+    for (int i = t; i < L - t; ++i) {
+      const int g = wrap(r0 - STEPS + i);
+      const f4 cur_old = v[i];
+      v[i] = axpy0(wprev[g], prev_old, wnext[g], v[i + 1]);
+      prev_old = cur_old;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const int r = r0 + i;
+    if (r < n_rows) __builtin_nontemporal_store(v[STEPS + i], reinterpret_cast<f4*>(Y + int64_t(r) * ldy) + c);
   }
 }
 
@@ -715,6 +759,41 @@ int dol_mix_dense_f32(const float* W, int64_t ldw, const float* X, int64_t ldx, 
   else if (vb) hipLaunchKernelGGL((dense_mix_mfma_kernel<false, true>), grid, dim3(256), 0, s, W, ldw, X, ldx, Y, ldy, M, K, P, nrt);
   else hipLaunchKernelGGL((dense_mix_mfma_kernel<false, false>), grid, dim3(256), 0, s, W, ldw, X, ldx, Y, ldy, M, K, P, nrt);
   return check_launch("dol_mix_dense_f32");
+}
+
+int dol_mix_ring_steps_f32(const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t n_rows,
+                           int64_t P, int32_t steps, const float* w_prev, const float* w_next,
+                           hipStream_t s) {
+  if (n_rows < 0 || P < 0 || steps < 0) return fail(DOL_EINVAL, "dol_mix_ring_steps_f32: negative size");
+  if (n_rows == 0 || P == 0) { g_err[0] = '\0'; return DOL_OK; }
+  if (!X || !Y || !w_prev || !w_next) return fail(DOL_EINVAL, "dol_mix_ring_steps_f32: null pointer");
+  if (ldx < P || ldy < P) return fail(DOL_EINVAL, "dol_mix_ring_steps_f32: ld < P");
+  if (X == Y) return fail(DOL_EINVAL, "dol_mix_ring_steps_f32: X and Y alias");
+  if (n_rows < 3) return fail(DOL_EINVAL, "dol_mix_ring_steps_f32: a ring needs n_rows >= 3");
+  if (steps == 0) return fail(DOL_EINVAL, "dol_mix_ring_steps_f32: steps must be >= 1");
+  const bool vec = row_vec_ok(X, ldx) && row_vec_ok(Y, ldy) && P % 4 == 0;
+  if (!vec || steps > 8) return fail(DOL_EINVAL, "dol_mix_ring_steps_f32: needs 16-B aligned rows, P %% 4 == 0 and steps <= 8 (compose launches otherwise)");
+  const int64_t n4 = P / 4;
+  const uint32_t nct = static_cast<uint32_t>(cdiv(n4, kThreads));
+  auto go = [&](auto steps_c, auto r_c) {
+    constexpr int S = decltype(steps_c)::value, R = decltype(r_c)::value;
+    const int64_t grid = int64_t(nct) * cdiv(n_rows, R);
+    if (grid > kMaxBlocks) return fail(DOL_EINVAL, "dol_mix_ring_steps_f32: too large");
+    hipLaunchKernelGGL((ring_steps_kernel<S, R>), dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, s, X, ldx, Y, ldy,
+                       n_rows, n4, nct, w_prev, w_next);
+    return check_launch("dol_mix_ring_steps_f32");
+  };
+  using std::integral_constant;
+  switch (steps) {
+    case 1: return go(integral_constant<int, 1>{}, integral_constant<int, 4>{});
+    case 2: return go(integral_constant<int, 2>{}, integral_constant<int, 8>{});
+    case 3: return go(integral_constant<int, 3>{}, integral_constant<int, 10>{});
+    case 4: return go(integral_constant<int, 4>{}, integral_constant<int, 12>{});
+    case 5: return go(integral_constant<int, 5>{}, integral_constant<int, 14>{});
+    case 6: return go(integral_constant<int, 6>{}, integral_constant<int, 16>{});
+    case 7: return go(integral_constant<int, 7>{}, integral_constant<int, 16>{});
+    default: return go(integral_constant<int, 8>{}, integral_constant<int, 16>{});
+  }
 }
 
 int dol_prox_admm_sgd_f32(float* w, int64_t ldw, float* buf, int64_t ldb, float* g, int64_t ldg,

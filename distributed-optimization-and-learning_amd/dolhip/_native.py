@@ -32,6 +32,7 @@ SIGNATURES = {
     "dol_version": [],
     "dol_last_error": [],
     "dol_mix_csr_f32": [_ptr, _i64, _i32, _ptr, _i64, _i32, _i64, _ptr, _ptr, _ptr, _ptr],
+    "dol_mix_ring_steps_f32": [_ptr, _i64, _ptr, _i64, _i32, _i64, _i32, _ptr, _ptr, _ptr],
     "dol_mix_dense_f32": [_ptr, _i64, _ptr, _i64, _ptr, _i64, _i32, _i32, _i64, _ptr],
     "dol_mix_ring_f32": [_ptr, _i64, _ptr, _i64, _i32, _i64, _ptr, _ptr, _ptr, _ptr, _ptr],
     "dol_prox_admm_sgd_f32": [_ptr, _i64, _ptr, _i64, _ptr, _i64, _ptr, _ptr, _i64, _f32, _f32, _f32,

@@ -149,11 +149,18 @@ class AgentBank:
         if a == "x" or b == "x":
             self.rebind_all()
 
-    def mix(self, plan, steps: int = 1) -> None:
-        """X <- W X, `steps` times (synchronous / Jacobi rounds)."""
+    def mix(self, plan, steps: int = 1, fuse: bool = True) -> None:
+        """X <- W X, `steps` times (synchronous / Jacobi rounds).  With `fuse`,
+        ring plans apply up to 8 rounds per HBM pass (temporal blocking,
+        bit-identical to single rounds)."""
         y = self.buffer("y")
-        for _ in range(steps):
-            plan.apply(self.buffer("x"), y, P=self.P)
+        done = 0
+        while done < steps:
+            if fuse:
+                done += plan.apply_steps(self.buffer("x"), y, steps - done, P=self.P)
+            else:
+                plan.apply(self.buffer("x"), y, P=self.P)
+                done += 1
             self._buf["x"], self._buf["y"] = y, self._buf["x"]
             y = self._buf["y"]
         self.rebind_all()

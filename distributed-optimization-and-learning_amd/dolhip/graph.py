@@ -255,6 +255,22 @@ class MixingPlan:
     def from_graph(cls, W: Graph, device, allow_ring: bool = True, dense: bool = False) -> "MixingPlan":
         return cls(csr_from_dense(W), device, allow_ring, dense)
 
+    MAX_FUSED_STEPS = 8
+
+    def apply_steps(self, X: torch.Tensor, Y: torch.Tensor, steps: int, P: Optional[int] = None) -> int:
+        """Apply up to `steps` synchronous rounds in one pass when the plan and
+        layout allow (ring, P % 4 == 0, 16-B aligned rows); returns how many
+        rounds were applied (>= 1).  Bit-identical to single rounds."""
+        P = X.shape[1] if P is None else P
+        k = min(int(steps), self.MAX_FUSED_STEPS)
+        if (k > 1 and self.kind == "ring" and P % 4 == 0 and X.data_ptr() % 16 == 0 and Y.data_ptr() % 16 == 0
+                and X.stride(0) % 4 == 0 and Y.stride(0) % 4 == 0):
+            from . import ops
+            ops.mix_ring_steps(X, Y, self.w_prev, self.w_next, k, P=P, n_rows=self.n_rows)
+            return k
+        self.apply(X, Y, P=P)
+        return 1
+
     def apply(self, X: torch.Tensor, Y: torch.Tensor, P: Optional[int] = None) -> torch.Tensor:
         from . import ops
         if self.kind == "ring":

@@ -14,7 +14,7 @@ from . import _native
 from ._native import DolNativeError
 
 __all__ = [
-    "DolNativeError", "mix_csr", "mix_ring", "mix_dense", "prox_admm_sgd", "admm_dual", "ordered_mean",
+    "DolNativeError", "mix_csr", "mix_ring", "mix_dense", "mix_ring_steps", "prox_admm_sgd", "admm_dual", "ordered_mean",
     "ordered_sum", "stream_copy", "dual_workspace_bytes", "prox_grad",
 ]
 
@@ -75,6 +75,24 @@ def mix_csr(X: torch.Tensor, Y: torch.Tensor, rowptr: torch.Tensor, col: torch.T
     _native.call("dol_mix_csr_f32", X.data_ptr(), ldx, X.shape[0], Y.data_ptr(), ldy, n, P,
                  rowptr.data_ptr(), col.data_ptr() if col.numel() else None,
                  val.data_ptr() if val.numel() else None, _stream(X))
+    return Y
+
+
+def mix_ring_steps(X: torch.Tensor, Y: torch.Tensor, w_prev: torch.Tensor, w_next: torch.Tensor, steps: int,
+                   P: Optional[int] = None, n_rows: Optional[int] = None) -> torch.Tensor:
+    """Y = W^steps X for the wrap-around ring in one HBM pass (bit-identical to
+    `steps` mix_ring calls).  Needs P % 4 == 0 and 16-B aligned rows."""
+    P = X.shape[1] if P is None else P
+    n = X.shape[0] if n_rows is None else n_rows
+    ldx = _check_rows("X", X, P)
+    ldy = _check_rows("Y", Y, P)
+    for nm, t in (("w_prev", w_prev), ("w_next", w_next)):
+        if t.device != X.device or t.dtype != torch.float32 or t.numel() < n or not t.is_contiguous():
+            raise ValueError(f"{nm}: expected contiguous float32 [{n}] on {X.device}")
+    if X.data_ptr() == Y.data_ptr():
+        raise ValueError("X and Y alias")
+    _native.call("dol_mix_ring_steps_f32", X.data_ptr(), ldx, Y.data_ptr(), ldy, n, P, int(steps),
+                 w_prev.data_ptr(), w_next.data_ptr(), _stream(X))
     return Y
 
 

@@ -76,6 +76,19 @@ int dol_mix_ring_f32(const float* X, int64_t ldx, float* Y, int64_t ldy,
                      hipStream_t s);
 
 /*
+ * `steps` synchronous ring rounds in ONE pass over HBM (temporal blocking):
+ * Y = W^steps X for the wrap-around ring of dol_mix_ring_f32, replacing the
+ * eps consensus steps of FedLCon.run (DIST/simulators.py:190-196; the
+ * reference applies Neighbors + consensus + load_state_dict eps times).
+ * Each intermediate value is computed with the single-round formula, so Y is
+ * bit-identical to `steps` calls of dol_mix_ring_f32 (ping-ponging buffers).
+ * Requires 16-B aligned rows, P % 4 == 0, n_rows >= 3, 1 <= steps <= 8.
+ */
+int dol_mix_ring_steps_f32(const float* X, int64_t ldx, float* Y, int64_t ldy,
+                           int32_t n_rows, int64_t P, int32_t steps,
+                           const float* w_prev, const float* w_next, hipStream_t s);
+
+/*
  * Dense mix on the matrix cores:  Y[M,P] = W[M,K] . X[K,P]   (fp32 MFMA)
  * For dense mixing matrices (communication_graph("compelete", ...), Erdos-
  * Renyi, time-varying W; DIST/simulators.py:54-58 and :59-64 with stochastic

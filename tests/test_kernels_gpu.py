@@ -331,3 +331,32 @@ def test_prox_grad_term_vs_oracle(admm, extra, gpu):
     ops.prox_grad(gd, padded(w, gpu, extra), dev(th, gpu), 0.1, alpha=padded(al, gpu, extra) if admm else None, P=P)
     torch.cuda.synchronize()
     assert bits_equal(gd[:, :P].cpu().numpy(), oracle.prox_grad(g, w, th, al, 0.1))
+
+
+@pytest.mark.parametrize("steps", [1, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("n,P", [(3, 8), (17, 4100), (64, 1024 * 5)])
+def test_ring_steps_bit_identical_to_single_rounds(steps, n, P, gpu):
+    rng = np.random.default_rng(steps * 100 + n)
+    X = rng.standard_normal((n, P)).astype(np.float32)
+    wp, wn = rng.random(n).astype(np.float32), rng.random(n).astype(np.float32)
+    want = X
+    for _ in range(steps):
+        want = oracle.mix_ring(want, wp, wn)
+    Y = torch.empty(n, P, device=gpu)
+    ops.mix_ring_steps(dev(X, gpu), Y, dev(wp, gpu), dev(wn, gpu), steps)
+    torch.cuda.synchronize()
+    assert bits_equal(Y.cpu().numpy(), want)
+
+
+def test_bank_mix_fused_equals_unfused(gpu):
+    from dolhip.bank import AgentBank
+    torch.manual_seed(5)
+    W = G.communication_graph("circle", "stochastic", 33)[0]
+    plan = G.MixingPlan.from_graph(W, gpu)
+    X = torch.randn(33, 2048, device=gpu)
+    a, b = AgentBank(33, 2048, gpu), AgentBank(33, 2048, gpu)
+    a.rows()[:] = X
+    b.rows()[:] = X
+    a.mix(plan, steps=13, fuse=True)     # 8 + 5 fused
+    b.mix(plan, steps=13, fuse=False)    # 13 single rounds
+    assert bits_equal(a.rows().cpu().numpy(), b.rows().cpu().numpy())
