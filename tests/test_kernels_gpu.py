@@ -360,3 +360,17 @@ def test_bank_mix_fused_equals_unfused(gpu):
     a.mix(plan, steps=13, fuse=True)     # 8 + 5 fused
     b.mix(plan, steps=13, fuse=False)    # 13 single rounds
     assert bits_equal(a.rows().cpu().numpy(), b.rows().cpu().numpy())
+
+
+@pytest.mark.parametrize("n,deg,P", [(600, 4, 1024 * 8 + 12), (2048, 6, 4096), (513, 2, 128 + 4 * 32 + 3)])
+def test_mix_csr_xcd_path_vs_oracle(n, deg, P, gpu):
+    """Large graphs take the XCD-pinned 512-B-tile path (plus the 4 KiB-tile
+    remainder and the scalar tail)."""
+    c = G.random_regular_csr(n, deg, seed=n + 1)
+    rng = np.random.default_rng(2)
+    X = rng.standard_normal((n, P)).astype(np.float32)
+    plan = G.MixingPlan(c, gpu)
+    Yd = torch.empty(n, P, device=gpu)
+    plan.apply(dev(X, gpu), Yd)
+    torch.cuda.synchronize()
+    assert bits_equal(Yd.cpu().numpy(), oracle.mix_csr(X, c.rowptr, c.col, c.val))
