@@ -113,9 +113,9 @@ def cpu_baseline(n_agents: int, P: int, seconds: float, full_agents: int):
 
 def primal_dual_round(N: int, P: int, world: int, rank: int, device, steps: int):
     """Secondary measurement (BASELINE config 4, ADMM side): one FedADMM round
-    over ALL agents = fused ADMM-gradient + momentum-SGD step
-    (dol_prox_admm_sgd_f32, DEC/clients.py:125-139 + SGD.step), dual ascent
-    (dol_admm_dual_f32, :141-144) and the global mean of the new weights
+    over ALL agents = the local step (ADMM gradient term + momentum SGD,
+    DEC/clients.py:125-139 + SGD.step) fused with the dual ascent that follows
+    it (:141-144) in dol_admm_step_dual_f32, then the global mean of the new weights
     (ordered sum of the local rows + all_reduce across ranks + /N,
     DEC/servers.py:42-48).  Timed like the headline (barrier, max over
     ranks); each kernel's share from HIP events."""
@@ -129,7 +129,7 @@ def primal_dual_round(N: int, P: int, world: int, rank: int, device, steps: int)
         t.normal_(generator=g)
     theta = torch.empty(ld, dtype=torch.float32, device=device).normal_(generator=g)
     order = torch.arange(n, dtype=torch.int32, device=device)
-    names = ("sgd", "dual", "mean")
+    names = ("step_dual", "mean")
     ev = {k: [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
           for k in names}
 
@@ -138,13 +138,10 @@ def primal_dual_round(N: int, P: int, world: int, rank: int, device, steps: int)
         def rec(nm, i):
             if e(nm):
                 e(nm)[i].record()
-        rec("sgd", 0)
-        ops.prox_admm_sgd(bufs["w"], bufs["g"], buf=bufs["mom"], theta=theta, alpha=bufs["alpha"], rho=0.1,
-                          lr=0.1, momentum=0.5, first_step=False, write_grad=False, P=P)
-        rec("sgd", 1)
-        rec("dual", 0)
-        ops.admm_dual(bufs["alpha"], bufs["w"], theta, 0.1, P=P)
-        rec("dual", 1)
+        rec("step_dual", 0)
+        ops.admm_step_dual(bufs["w"], bufs["g"], theta, bufs["alpha"], buf=bufs["mom"], rho=0.1, lr=0.1,
+                           momentum=0.5, first_step=False, write_grad=False, P=P)
+        rec("step_dual", 1)
         rec("mean", 0)
         parallel.global_mean(bufs["w"], order, N, P, out=theta)
         rec("mean", 1)
@@ -164,7 +161,8 @@ def primal_dual_round(N: int, P: int, world: int, rank: int, device, steps: int)
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     el = float(el.item())
     row_bytes = n * P * 4
-    alg = {"sgd": 6 * row_bytes, "dual": 3 * row_bytes, "mean": row_bytes + P * 4}  # compulsory bytes per launch
+    # compulsory bytes per launch: step+dual reads w, g, buf, alpha and writes w, buf, alpha
+    alg = {"step_dual": 7 * row_bytes, "mean": row_bytes + P * 4}
     kern = {}
     for nm in names:
         ms = float(np.mean([a.elapsed_time(b) for a, b in ev[nm]]))
@@ -175,7 +173,7 @@ def primal_dual_round(N: int, P: int, world: int, rank: int, device, steps: int)
     bufs.clear()
     torch.cuda.empty_cache()
     return {"rounds_per_s": steps / el, "ms_per_round": el / steps * 1e3, "agents": N, "params": P,
-            "what": "fused ADMM-grad+momentum-SGD step, dual ascent, global mean (all agents)",
+            "what": "ADMM-grad + momentum-SGD step fused with the dual ascent, then global mean (all agents)",
             "kernels": kern}
 
 

@@ -299,8 +299,8 @@ __global__ __launch_bounds__(kThreads) void csr_xcd_kernel(
 // Fused prox / ADMM gradient term + momentum SGD.
 // MODE: 0 = no momentum, 1 = momentum first step (buf = g'), 2 = momentum.
 // ----------------------------------------------------------------------------
-template <bool THETA, bool ALPHA, int MODE, bool WRITE_G>
-__device__ __forceinline__ void prox_sgd_lane(float& w, float& bf, float& g, float th, float al,
+template <bool THETA, bool ALPHA, int MODE, bool WRITE_G, bool DUAL = false>
+__device__ __forceinline__ void prox_sgd_lane(float& w, float& bf, float& g, float th, float& al,
                                               float rho, float neg_lr, float mom) {
   float gg = g;
   if constexpr (THETA) {
@@ -313,12 +313,13 @@ __device__ __forceinline__ void prox_sgd_lane(float& w, float& bf, float& g, flo
   if constexpr (MODE == 1) { bf = gg; d = gg; }
   if constexpr (MODE == 2) { bf = bf * mom + gg; d = bf; }
   w = __builtin_fmaf(neg_lr, d, w);
+  if constexpr (DUAL) al = al + rho * (w - th);  // update_duals on the new w (DEC/clients.py:141-144)
 }
 
-template <typename V, bool THETA, bool ALPHA, int MODE, bool WRITE_G>
+template <typename V, bool THETA, bool ALPHA, int MODE, bool WRITE_G, bool DUAL = false>
 __global__ __launch_bounds__(kThreads) void prox_sgd_kernel(
     float* __restrict__ W, int64_t ldw, float* __restrict__ B, int64_t ldb, float* __restrict__ G,
-    int64_t ldg, const float* __restrict__ theta, const float* __restrict__ A, int64_t lda,
+    int64_t ldg, const float* __restrict__ theta, float* __restrict__ A, int64_t lda,
     float rho, float neg_lr, float mom, int64_t c_off, int64_t ncols_v, int64_t n_col_tiles) {
   const int64_t blk = blockIdx.x;
   const int64_t agent = blk / n_col_tiles;
@@ -332,20 +333,22 @@ __global__ __launch_bounds__(kThreads) void prox_sgd_kernel(
   if constexpr (THETA) th = *(reinterpret_cast<const V*>(theta + c_off) + c);
   if constexpr (ALPHA) al = *(reinterpret_cast<const V*>(A + agent * lda + c_off) + c);
   if constexpr (Vec<V>::W == 1) {
-    prox_sgd_lane<THETA, ALPHA, MODE, WRITE_G>(w, bf, g, th, al, rho, neg_lr, mom);
+    prox_sgd_lane<THETA, ALPHA, MODE, WRITE_G, DUAL>(w, bf, g, th, al, rho, neg_lr, mom);
   } else {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      float wj = w[j], bj = bf[j], gj = g[j];
-      prox_sgd_lane<THETA, ALPHA, MODE, WRITE_G>(wj, bj, gj, th[j], al[j], rho, neg_lr, mom);
+      float wj = w[j], bj = bf[j], gj = g[j], aj = al[j];
+      prox_sgd_lane<THETA, ALPHA, MODE, WRITE_G, DUAL>(wj, bj, gj, th[j], aj, rho, neg_lr, mom);
       w[j] = wj;
       bf[j] = bj;
       g[j] = gj;
+      al[j] = aj;
     }
   }
   *wp = w;
   if constexpr (WRITE_G) *gp = g;
   if constexpr (MODE != 0) *(reinterpret_cast<V*>(B + agent * ldb + c_off) + c) = bf;
+  if constexpr (DUAL) *(reinterpret_cast<V*>(A + agent * lda + c_off) + c) = al;
 }
 
 // Gradient term alone: g += rho*(w - theta) (+ alpha), w untouched.
@@ -690,9 +693,10 @@ void launch_prox(float* w, int64_t ldw, float* b, int64_t ldb, float* g, int64_t
                  const float* th, const float* a, int64_t lda, float rho, float lr, float mom,
                  int n_agents, int64_t c_off, int64_t ncols_v, hipStream_t s) {
   const int64_t n_col_tiles = cdiv(ncols_v, kThreads);
+  // alpha is only read on this path (the kernel's pointer is non-const for the fused-dual variant)
   hipLaunchKernelGGL((prox_sgd_kernel<V, TH, AL, MODE, WG>), dim3(static_cast<unsigned>(n_col_tiles * n_agents)),
-                     dim3(kThreads), 0, s, w, ldw, b, ldb, g, ldg, th, a, lda, rho, -lr, mom, c_off,
-                     ncols_v, n_col_tiles);
+                     dim3(kThreads), 0, s, w, ldw, b, ldb, g, ldg, th, const_cast<float*>(a), lda, rho, -lr, mom,
+                     c_off, ncols_v, n_col_tiles);
 }
 
 template <typename V, bool TH, bool AL, int MODE>
@@ -882,6 +886,41 @@ int dol_prox_admm_sgd_f32(float* w, int64_t ldw, float* buf, int64_t ldb, float*
     dispatch_prox<float>(th, al, mode, wg, w, ldw, buf, ldb, g, ldg, theta, alpha, lda, rho, lr,
                          momentum, n_agents, cs.n4 * 4, cs.tail, s);
   return check_launch("dol_prox_admm_sgd_f32");
+}
+
+int dol_admm_step_dual_f32(float* w, int64_t ldw, float* buf, int64_t ldb, float* g, int64_t ldg,
+                           const float* theta, float* alpha, int64_t lda, float rho, float lr,
+                           float momentum, int first_step, int write_grad, int32_t n_agents, int64_t P,
+                           hipStream_t s) {
+  if (n_agents < 0 || P < 0) return fail(DOL_EINVAL, "dol_admm_step_dual_f32: negative size");
+  if (n_agents == 0 || P == 0) { g_err[0] = '\0'; return DOL_OK; }
+  if (!w || !g || !theta || !alpha) return fail(DOL_EINVAL, "dol_admm_step_dual_f32: null pointer");
+  const int mode = (momentum == 0.0f) ? 0 : (first_step ? 1 : 2);
+  if (mode != 0 && !buf) return fail(DOL_EINVAL, "dol_admm_step_dual_f32: momentum needs buf");
+  if (ldw < P || ldg < P || lda < P || (mode != 0 && ldb < P)) return fail(DOL_EINVAL, "dol_admm_step_dual_f32: ld < P");
+  const bool vec_ok = row_vec_ok(w, ldw) && row_vec_ok(g, ldg) && (mode == 0 || row_vec_ok(buf, ldb)) &&
+                      row_vec_ok(theta, 0) && row_vec_ok(alpha, lda);
+  const ColSplit cs = split_cols(P, vec_ok);
+  if (cdiv(cs.n4 + cs.tail, kThreads) * n_agents > kMaxBlocks) return fail(DOL_EINVAL, "dol_admm_step_dual_f32: too large");
+  auto launch = [&](auto vtag, auto mode_c, auto wg_c, int64_t c_off, int64_t nc) {
+    using V = decltype(vtag);
+    constexpr int M = decltype(mode_c)::value;
+    constexpr bool WG = decltype(wg_c)::value;
+    const int64_t nct = cdiv(nc, kThreads);
+    hipLaunchKernelGGL((prox_sgd_kernel<V, true, true, M, WG, true>), dim3(static_cast<unsigned>(nct * n_agents)),
+                       dim3(kThreads), 0, s, w, ldw, buf, ldb, g, ldg, theta, alpha, lda, rho, -lr, momentum, c_off,
+                       nc, nct);
+  };
+  auto by_mode = [&](auto vtag, int64_t c_off, int64_t nc) {
+    using std::integral_constant;
+    const bool wg = write_grad != 0;
+    if (mode == 0) { if (wg) launch(vtag, integral_constant<int, 0>{}, std::true_type{}, c_off, nc); else launch(vtag, integral_constant<int, 0>{}, std::false_type{}, c_off, nc); }
+    else if (mode == 1) { if (wg) launch(vtag, integral_constant<int, 1>{}, std::true_type{}, c_off, nc); else launch(vtag, integral_constant<int, 1>{}, std::false_type{}, c_off, nc); }
+    else { if (wg) launch(vtag, integral_constant<int, 2>{}, std::true_type{}, c_off, nc); else launch(vtag, integral_constant<int, 2>{}, std::false_type{}, c_off, nc); }
+  };
+  if (cs.n4 > 0) by_mode(f4{}, 0, cs.n4);
+  if (cs.tail > 0) by_mode(float{}, cs.n4 * 4, cs.tail);
+  return check_launch("dol_admm_step_dual_f32");
 }
 
 int dol_prox_grad_f32(float* g, int64_t ldg, const float* w, int64_t ldw, const float* theta,

@@ -15,7 +15,7 @@ from ._native import DolNativeError
 
 __all__ = [
     "DolNativeError", "mix_csr", "mix_ring", "mix_dense", "mix_ring_steps", "prox_admm_sgd", "admm_dual", "ordered_mean",
-    "ordered_sum", "stream_copy", "dual_workspace_bytes", "prox_grad",
+    "ordered_sum", "stream_copy", "dual_workspace_bytes", "prox_grad", "admm_step_dual",
 ]
 
 
@@ -167,6 +167,29 @@ def prox_admm_sgd(w: torch.Tensor, g: torch.Tensor, buf: Optional[torch.Tensor] 
     _check_vec("theta", theta, P, w.device)
     _native.call("dol_prox_admm_sgd_f32", w.data_ptr(), ldw, _ptr(buf) if momentum != 0.0 else None, ldb,
                  g.data_ptr(), ldg, _ptr(theta), _ptr(alpha), lda, float(rho), float(lr), float(momentum),
+                 int(bool(first_step)), int(bool(write_grad)), n, P, _stream(w))
+
+
+def admm_step_dual(w: torch.Tensor, g: torch.Tensor, theta: torch.Tensor, alpha: torch.Tensor,
+                   buf: Optional[torch.Tensor] = None, rho: float = 0.0, lr: float = 0.01, momentum: float = 0.0,
+                   first_step: bool = False, write_grad: bool = True, P: Optional[int] = None) -> None:
+    """Last FedADMM local step + dual ascent in one pass (bit-identical to
+    prox_admm_sgd(theta, alpha) followed by admm_dual)."""
+    P = w.shape[1] if P is None else P
+    n = w.shape[0]
+    ldw = _check_rows("w", w, P)
+    ldg = _check_rows("g", g, P)
+    lda = _check_rows("alpha", alpha, P)
+    if g.shape[0] < n or alpha.shape[0] < n:
+        raise ValueError("g/alpha have fewer rows than w")
+    ldb = 0
+    if momentum != 0.0:
+        if buf is None:
+            raise ValueError("momentum != 0 needs buf")
+        ldb = _check_rows("buf", buf, P)
+    _check_vec("theta", theta, P, w.device)
+    _native.call("dol_admm_step_dual_f32", w.data_ptr(), ldw, _ptr(buf) if momentum != 0.0 else None, ldb,
+                 g.data_ptr(), ldg, theta.data_ptr(), alpha.data_ptr(), lda, float(rho), float(lr), float(momentum),
                  int(bool(first_step)), int(bool(write_grad)), n, P, _stream(w))
 
 

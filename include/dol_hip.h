@@ -125,6 +125,19 @@ int dol_prox_admm_sgd_f32(float* w, int64_t ldw, float* buf, int64_t ldb,
                           int32_t n_agents, int64_t P, hipStream_t s);
 
 /*
+ * The LAST local FedADMM step of a round fused with the dual ascent, one pass:
+ *   dol_prox_admm_sgd_f32(theta, alpha)  then  alpha = fl(alpha + fl(rho*fl(w' - theta)))
+ * on the updated w' (DEC/clients.py:125-139, SGD.step, then update_duals
+ * :141-144 called at :52).  Bit-identical to the two calls in sequence; reads
+ * w, g, buf, alpha once and writes w, buf, alpha (and g if write_grad).
+ */
+int dol_admm_step_dual_f32(float* w, int64_t ldw, float* buf, int64_t ldb,
+                           float* g, int64_t ldg, const float* theta,
+                           float* alpha, int64_t lda, float rho, float lr,
+                           float momentum, int first_step, int write_grad,
+                           int32_t n_agents, int64_t P, hipStream_t s);
+
+/*
  * The proximal / ADMM gradient term alone, in place (no optimizer step):
  *   FedProx_Client.update_model  DEC/clients.py:108-111  g = fl(g + fl(rho*fl(w-theta)))
  *   FedAdmm_Client.update_model  DEC/clients.py:132-135  g = fl(g + fl(alpha + fl(rho*fl(w-theta))))

@@ -374,3 +374,22 @@ def test_mix_csr_xcd_path_vs_oracle(n, deg, P, gpu):
     plan.apply(dev(X, gpu), Yd)
     torch.cuda.synchronize()
     assert bits_equal(Yd.cpu().numpy(), oracle.mix_csr(X, c.rowptr, c.col, c.val))
+
+
+@pytest.mark.parametrize("mom,first", [(0.0, False), (0.5, True), (0.5, False)])
+@pytest.mark.parametrize("extra", [0, 1])
+def test_admm_step_dual_equals_two_calls(mom, first, extra, gpu):
+    rng = np.random.default_rng(31)
+    n, P = 4, 30001
+    w, g, b, al = (rng.standard_normal((n, P)).astype(np.float32) for _ in range(4))
+    th = rng.standard_normal(P).astype(np.float32)
+    wd, gd, bd, ad = (padded(a, gpu, extra) for a in (w, g, b, al))
+    ops.admm_step_dual(wd, gd, dev(th, gpu), ad, buf=bd, rho=0.1, lr=0.05, momentum=mom, first_step=first, P=P)
+    torch.cuda.synchronize()
+    w1, b1, g1 = oracle.prox_admm_sgd(w, b, g, th, al, 0.1, 0.05, mom, first)
+    a1, _ = oracle.admm_dual(al, w1, th, 0.1)
+    assert bits_equal(wd[:, :P].cpu().numpy(), w1)
+    assert bits_equal(ad[:, :P].cpu().numpy(), a1)
+    assert bits_equal(gd[:, :P].cpu().numpy(), g1)
+    if mom != 0:
+        assert bits_equal(bd[:, :P].cpu().numpy(), b1)
