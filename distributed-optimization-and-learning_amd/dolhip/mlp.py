@@ -1,0 +1,87 @@
+"""Batched per-agent MLP local steps (BASELINE config 5).
+
+N agents each own a `nn.Sequential(Linear(d, h), ReLU(), Linear(h, c))`
+whose parameters are rows of an AgentBank (state_dict order: 0.weight [h,d],
+0.bias [h], 2.weight [c,h], 2.bias [c]).  One local step for ALL agents:
+
+  Z1 = X W1^T + b1,  H = relu(Z1),  Z2 = H W2^T + b2,  loss = CE(Z2, y)  (mean over the batch)
+  dZ2 = (softmax(Z2) - onehot(y)) / B
+  dW2 = dZ2^T H,  db2 = sum_b dZ2,  dH = dZ2 W2,  dZ1 = dH * [Z1 > 0]
+  dW1 = dZ1^T X,  db1 = sum_b dZ1
+  then one fused SGD / prox / ADMM kernel over every row (dol_prox_admm_sgd_f32)
+
+The GEMMs are strided-batched over the bank rows (batch stride = ld): the
+weights are read in place and dW1/dW2 are written straight into the bank's
+grad rows, no copies.  This is the per-agent loop of DIST/clients.py:34-59
+(one nn.Module forward/backward per agent) batched into one launch per layer.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from .bank import AgentBank
+
+
+def mlp_layout(d: int, h: int, c: int):
+    return [("0.weight", (h, d)), ("0.bias", (h,)), ("2.weight", (c, h)), ("2.bias", (c,))]
+
+
+class BatchedMLP:
+    def __init__(self, bank: AgentBank, d: int, h: int, c: int):
+        if [k for k, *_ in bank.offsets] != ["0.weight", "0.bias", "2.weight", "2.bias"]:
+            raise ValueError("bank layout must be mlp_layout(d, h, c)")
+        self.bank, self.d, self.h, self.c = bank, d, h, c
+        self.off = {k: o for k, o, _, _ in bank.offsets}
+
+    def _views(self, name: str):
+        t = self.bank.buffer(name, zero=(name == "grad"))
+        n, d, h, c, o = self.bank.n, self.d, self.h, self.c, self.off
+        W1 = t[:, o["0.weight"]:o["0.weight"] + h * d].view(n, h, d)
+        b1 = t[:, o["0.bias"]:o["0.bias"] + h]
+        W2 = t[:, o["2.weight"]:o["2.weight"] + c * h].view(n, c, h)
+        b2 = t[:, o["2.bias"]:o["2.bias"] + c]
+        return W1, b1, W2, b2
+
+    def init_like_torch(self, seed: int = 0) -> None:
+        """Default nn.Linear init per agent (same RNG order as constructing
+        N modules one after another)."""
+        g = torch.Generator().manual_seed(seed)
+        for i in range(self.bank.n):
+            torch.manual_seed(int(torch.randint(0, 2**31 - 1, (1,), generator=g)))
+            m = torch.nn.Sequential(torch.nn.Linear(self.d, self.h), torch.nn.ReLU(), torch.nn.Linear(self.h, self.c))
+            self.bank.load_module(i, m.to(self.bank.device))
+
+    def forward_backward(self, X: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+        """X [N, B, d] fp32, y [N, B] int64 on the bank's device.  Writes every
+        agent's gradient into the bank's grad rows; returns the per-agent mean
+        cross-entropy [N]."""
+        n, B = X.shape[0], X.shape[1]
+        if n != self.bank.n or X.shape[2] != self.d:
+            raise ValueError(f"X must be [{self.bank.n}, B, {self.d}]")
+        W1, b1, W2, b2 = self._views("x")
+        gW1, gb1, gW2, gb2 = self._views("grad")
+        with torch.no_grad():
+            Z1 = torch.baddbmm(b1.unsqueeze(1), X, W1.transpose(1, 2))        # [n, B, h]
+            H = torch.relu(Z1)
+            Z2 = torch.baddbmm(b2.unsqueeze(1), H, W2.transpose(1, 2))        # [n, B, c]
+            logp = torch.log_softmax(Z2, dim=2)
+            loss = -logp.gather(2, y.unsqueeze(2)).squeeze(2).mean(1)         # [n]
+            dZ2 = torch.exp(logp)
+            dZ2.scatter_add_(2, y.unsqueeze(2), torch.full_like(logp[..., :1], -1.0))
+            dZ2.mul_(1.0 / B)
+            torch.bmm(dZ2.transpose(1, 2), H, out=gW2)                        # [n, c, h] into grad rows
+            torch.sum(dZ2, dim=1, out=gb2)
+            dH = torch.bmm(dZ2, W2)                                           # [n, B, h]
+            dZ1 = dH.mul_(Z1 > 0)
+            torch.bmm(dZ1.transpose(1, 2), X, out=gW1)                        # [n, h, d] into grad rows
+            torch.sum(dZ1, dim=1, out=gb1)
+        return loss
+
+    def step(self, X: torch.Tensor, y: torch.Tensor, lr: float, momentum: float, first_step: bool,
+             theta: Optional[torch.Tensor] = None, rho: float = 0.0, admm: bool = False) -> torch.Tensor:
+        loss = self.forward_backward(X, y)
+        self.bank.local_step(lr=lr, momentum=momentum, first_step=first_step, theta=theta, rho=rho, admm=admm,
+                             write_grad=False)
+        return loss

@@ -32,6 +32,58 @@ def time_plan(plan, X, Y, P, reps):
     return s.elapsed_time(e) / reps
 
 
+def mlp_round(N, d, h, c, B, p_edge, reps, dev):
+    """BASELINE config 5: Erdos-Renyi W (dense, MFMA) mixing + one batched MLP local step per round."""
+    from dolhip.bank import AgentBank
+    from dolhip.mlp import BatchedMLP, mlp_layout
+    bank = AgentBank(N, mlp_layout(d, h, c), dev)
+    mlp = BatchedMLP(bank, d, h, c)
+    bank.buffer("x").normal_(0, 0.05)
+    bank.buffer("y").zero_()
+    bank.buffer("mom", zero=True)
+    gen = torch.Generator().manual_seed(2028)
+    A = (torch.rand(N, N, generator=gen) < p_edge).float()
+    A.fill_diagonal_(0)
+    R = torch.rand(N, N, generator=gen) * A
+    R /= R.sum(0).clamp_min(1e-30)
+    plan = G.MixingPlan.from_graph(R.T.contiguous(), dev, dense=True)
+    X = torch.randn(N, B, d, device=dev)
+    y = torch.randint(0, c, (N, B), device=dev)
+    ev = {k: [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+          for k in ("fwd_bwd", "sgd", "mix")}
+
+    def one(k=None):
+        r = (lambda nm, i: ev[nm][k][i].record()) if k is not None else (lambda nm, i: None)
+        r("fwd_bwd", 0)
+        mlp.forward_backward(X, y)
+        r("fwd_bwd", 1)
+        r("sgd", 0)
+        bank.local_step(lr=0.05, momentum=0.5, first_step=False, write_grad=False)
+        r("sgd", 1)
+        r("mix", 0)
+        bank.mix(plan)
+        r("mix", 1)
+    for _ in range(2):
+        one()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(reps):
+        one(k)
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) / reps
+    ms = {k: sum(a.elapsed_time(b) for a, b in v) / reps for k, v in ev.items()}
+    P = bank.P
+    flops_fb = 2.0 * N * B * (d * h + h * c) * 3  # fwd + two backward GEMMs per layer
+    out = {"workload": "config5: ER p=%.2f dense MFMA mix + batched MLP %d-%d-%d local step" % (p_edge, d, h, c),
+           "agents": N, "params": P, "batch": B, "ms_per_round": el * 1e3, "rounds_per_s": 1 / el, "kernel_ms": ms,
+           "mix_TFLOPs": 2.0 * N * N * P / (ms["mix"] / 1e3) / 1e12,
+           "fwd_bwd_TFLOPs": flops_fb / (ms["fwd_bwd"] / 1e3) / 1e12,
+           "sgd_GBps": 5 * N * P * 4 / (ms["sgd"] / 1e3) / 1e9}
+    print(json.dumps(out), flush=True)
+    del bank, mlp, plan, X, y
+    torch.cuda.empty_cache()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--agents", type=int, nargs="+", default=[1024, 8192])
@@ -39,9 +91,12 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--topologies", nargs="+", default=["ring", "ring-eps5", "rr4", "dense-er0.1"])
     ap.add_argument("--dense-max-agents", type=int, default=2048)
+    ap.add_argument("--mlp", type=int, nargs="*", default=[1024], help="agent counts for the config-5 MLP round")
     a = ap.parse_args()
     dev = torch.device("cuda")
     P = a.params
+    for N in a.mlp:
+        mlp_round(N, 784, 128, 10, 32, 0.1, a.reps, dev)
     for N in a.agents:
         ld = row_stride(P)
         X = torch.empty(N, ld, device=dev).normal_()
