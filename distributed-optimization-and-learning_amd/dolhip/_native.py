@@ -74,8 +74,19 @@ def lib():
     return _lib
 
 
+_TRACE = os.environ.get("DOL_TRACE", "") not in ("", "0")
+
+
 def call(name: str, *args) -> None:
-    rc = getattr(lib(), name)(*args)
+    if _TRACE:  # roctx range per C-ABI call (visible in rocprofv3 --marker-trace)
+        import torch
+        torch.cuda.nvtx.range_push(name)
+        try:
+            rc = getattr(lib(), name)(*args)
+        finally:
+            torch.cuda.nvtx.range_pop()
+    else:
+        rc = getattr(lib(), name)(*args)
     if rc != 0:
         msg = lib().dol_last_error().decode(errors="replace")
         raise DolNativeError(f"{name} returned {rc}: {msg}")

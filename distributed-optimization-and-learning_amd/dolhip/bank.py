@@ -188,6 +188,25 @@ class AgentBank:
         idx = torch.as_tensor(list(order), dtype=torch.int32, device=self.device)
         return ops.ordered_mean(self.buffer(name), idx, out=out, P=self.P)
 
+    # ------------------------------------------------------------------ checkpoint / resume
+    def save(self, path: str, names: Iterable[str] = ("x", "mom", "alpha")) -> None:
+        """Write the stacked state (unpadded [N, P] per buffer) with safetensors
+        (no pickles).  The reference keeps no model checkpoints."""
+        from safetensors.torch import save_file
+        tensors = {n: self.rows(n).contiguous().cpu() for n in names if self.has(n)}
+        meta = {"P": str(self.P), "n": str(self.n), "layout": repr(self.layout)}
+        save_file(tensors, path, metadata=meta)
+
+    def load(self, path: str) -> None:
+        from safetensors import safe_open
+        with safe_open(path, framework="pt") as f:
+            meta = f.metadata() or {}
+            if int(meta.get("P", self.P)) != self.P or int(meta.get("n", self.n)) != self.n:
+                raise ValueError(f"checkpoint is [{meta.get('n')}, {meta.get('P')}], bank is [{self.n}, {self.P}]")
+            for name in f.keys():
+                self.buffer(name, zero=True)[:, : self.P].copy_(f.get_tensor(name))
+        self.rebind_all()
+
     def unflatten(self, vec: torch.Tensor) -> Dict[str, torch.Tensor]:
         return {k: vec[o:o + c].view(shape) for k, o, c, shape in self.offsets}
 

@@ -158,3 +158,15 @@ def test_unfused_update_model_path_equals_fused(gpu):
         srv.run(0.3, 1)
     assert oracle.bits_equal(fast.bank.rows().cpu().numpy(), slow.bank.rows().cpu().numpy())
     assert oracle.bits_equal(fast.bank.rows("alpha").cpu().numpy(), slow.bank.rows("alpha").cpu().numpy())
+
+
+def test_bank_checkpoint_roundtrip(gpu, tmp_path):
+    from dolhip.bank import AgentBank
+    a = AgentBank(5, [("w", (3, 7)), ("b", (11,))], gpu)
+    a.rows()[:] = torch.randn(5, a.P, device=gpu)
+    a.buffer("mom", zero=True)[:, : a.P] = torch.randn(5, a.P, device=gpu)
+    p = str(tmp_path / "bank.safetensors")
+    a.save(p)
+    b = AgentBank(5, [("w", (3, 7)), ("b", (11,))], gpu)
+    b.load(p)
+    assert torch.equal(a.rows(), b.rows()) and torch.equal(a.rows("mom"), b.rows("mom"))

@@ -86,7 +86,7 @@ def mlp_round(N, d, h, c, B, p_edge, reps, dev):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--agents", type=int, nargs="+", default=[1024, 8192])
+    ap.add_argument("--agents", type=int, nargs="*", default=[1024, 8192])
     ap.add_argument("--params", type=int, default=1 << 20)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--topologies", nargs="+", default=["ring", "ring-eps5", "rr4", "dense-er0.1"])
