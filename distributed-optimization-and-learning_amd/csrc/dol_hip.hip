@@ -168,6 +168,52 @@ __global__ __launch_bounds__(kThreads) void ring_mix_kernel(
 }
 
 
+
+// LDS-DMA form of the ring mix (the default float4 path).  Each wave moves
+// its 1 KiB quarter of the tile's R + 2 rows straight into LDS with
+// global_load_lds_dwordx4 (default cache policy: the halo rows' second reads
+// must hit L2), waits on its own vmcnt, reads its lanes back and stores with
+// nontemporal stores.  No barrier: a wave only reads what it loaded.  On
+// MI355X (tools/membench7/8.hip, same box): 6.17 TB/s vs 5.91 for the
+// register-staged kernel, = the measured copy ceiling (6.16); nt loads here
+// cost 17 % (they evict the halo rows from L2).
+#define DOL_GPTR(p) ((const __attribute__((address_space(1))) void*)(p))
+#define DOL_LPTR(p) ((__attribute__((address_space(3))) void*)(p))
+
+template <int R>
+__global__ __launch_bounds__(kThreads) void ring_mix_dma_kernel(
+    const float* __restrict__ X, int64_t ldx, float* __restrict__ Y, int64_t ldy, int n_rows,
+    int64_t ncols_v, int64_t n_col_tiles, const float* __restrict__ halo_prev,
+    const float* __restrict__ halo_next, const float* __restrict__ wprev, const float* __restrict__ wnext) {
+  __shared__ __attribute__((aligned(16))) float lds[kThreads / 64][R + 2][256];
+  const uint32_t b = blockIdx.x;
+  const uint32_t nct = static_cast<uint32_t>(n_col_tiles);
+  const uint32_t ct = b % nct;
+  const int r0 = static_cast<int>(b / nct) * R;
+  const int r1 = min(r0 + R, n_rows);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t c = int64_t(ct) * kThreads + threadIdx.x;  // f4 column
+  if (c >= ncols_v) return;
+  auto row = [&](int r) -> const float* {
+    return (r < 0) ? halo_prev : (r >= n_rows ? halo_next : X + int64_t(r) * ldx);
+  };
+#pragma unroll
+  for (int k = 0; k < R + 2; ++k) {
+    const int r = min(r0 - 1 + k, r1);
+    __builtin_amdgcn_global_load_lds(DOL_GPTR(row(r) + 4 * c), DOL_LPTR(&lds[wave][k][0]), 16, 0, 0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  f4 v[R + 2];
+#pragma unroll
+  for (int k = 0; k < R + 2; ++k) v[k] = *reinterpret_cast<const f4*>(&lds[wave][k][lane * 4]);
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    const int r = r0 + k;
+    if (r < r1)
+      __builtin_nontemporal_store(axpy0(wprev[r], v[k], wnext[r], v[k + 2]), reinterpret_cast<f4*>(Y + int64_t(r) * ldy) + c);
+  }
+}
+
 // ----------------------------------------------------------------------------
 // Temporally blocked ring mix: STEPS synchronous rounds in one HBM pass
 // (FedLCon's eps consensus steps, DIST/simulators.py:190-196).  A tile of R
@@ -791,10 +837,18 @@ int dol_mix_ring_f32(const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t
   const int pf = env_int("DOL_RING_PF", 4);
   const int nt = env_int("DOL_RING_NT", 2);
   if (cs.n4 > 0) {
-    const int rpb = ring_rows_per_block(n_rows, cdiv(cs.n4, kThreads), pf);
-    if (cdiv(cs.n4, kThreads) * cdiv(n_rows, rpb) > kMaxBlocks)
-      return fail(DOL_EINVAL, "dol_mix_ring_f32: problem too large for one launch");
-    launch_ring_variant<f4>(pf, nt, X, ldx, Y, ldy, n_rows, 0, cs.n4, rpb, halo_prev, halo_next, w_prev, w_next, s);
+    const int64_t nct = cdiv(cs.n4, kThreads);
+    if (env_int("DOL_RING_DMA", 1) != 0) {
+      constexpr int R = 4;
+      if (nct * cdiv(n_rows, R) > kMaxBlocks) return fail(DOL_EINVAL, "dol_mix_ring_f32: problem too large for one launch");
+      hipLaunchKernelGGL((ring_mix_dma_kernel<R>), dim3(static_cast<unsigned>(nct * cdiv(n_rows, R))), dim3(kThreads), 0, s,
+                         X, ldx, Y, ldy, n_rows, cs.n4, nct, halo_prev, halo_next, w_prev, w_next);
+    } else {
+      const int rpb = ring_rows_per_block(n_rows, nct, pf);
+      if (nct * cdiv(n_rows, rpb) > kMaxBlocks)
+        return fail(DOL_EINVAL, "dol_mix_ring_f32: problem too large for one launch");
+      launch_ring_variant<f4>(pf, nt, X, ldx, Y, ldy, n_rows, 0, cs.n4, rpb, halo_prev, halo_next, w_prev, w_next, s);
+    }
   }
   if (cs.tail > 0) {
     const int rpb = ring_rows_per_block(n_rows, cdiv(cs.tail, kThreads), 4);
