@@ -185,10 +185,16 @@ def main():
     if world != args.gpus:
         if rank == 0:
             print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
-    device = torch.device("cuda", local)
+    # DOL_DEVICE_MAP=0 puts every rank on cuda:0 and DOL_DIST_BACKEND=gloo stages
+    # halos through host memory: a rehearsal of the N>1 path on a 1-GPU box
+    device = torch.device("cuda", int(os.environ.get("DOL_DEVICE_MAP", local)))
     torch.cuda.set_device(device)
+    backend = os.environ.get("DOL_DIST_BACKEND", "nccl")
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(backend)
 
     import dolhip
     from dolhip.parallel import ShardedRing
@@ -280,11 +286,12 @@ def main():
                 "params": P,
                 "topology": "circle",
                 "mode": "stochastic",
-                "parallelism": f"agent-shard x{world}" + (" + RCCL halo send/recv" if world > 1 else ""),
+                "parallelism": f"agent-shard x{world}" + ((" + RCCL halo send/recv" if backend == "nccl" else
+                                                           f" + {backend} halo send/recv (rehearsal)") if world > 1 else ""),
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "ring_mix_kernel",
+                "kernel": "ring_mix_dma_kernel<4>" if os.environ.get("DOL_RING_DMA", "1") != "0" else "ring_mix_kernel",
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",

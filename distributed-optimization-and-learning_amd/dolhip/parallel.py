@@ -70,6 +70,10 @@ class ShardedRing:
         # optional (start, end) timing events recorded around the interior kernel
         self.kernel_events = None
 
+    def _staged(self) -> bool:
+        """gloo cannot send device tensors: stage the halo rows through host memory."""
+        return self.device.type == "cuda" and dist.get_backend(self.group) == "gloo"
+
     def _exchange(self, x: torch.Tensor):
         """Post the halo send/recv pairs; returns the requests.
 
@@ -78,13 +82,25 @@ class ShardedRing:
         then the 'upstream' one (my first row -> prev rank's halo_next)."""
         P = self.P
         first, last = x[0, :P], x[self.n_local - 1, :P]
+        hp, hn = self.halo_prev[:P], self.halo_next[:P]
+        if self._staged():
+            first, last = first.cpu(), last.cpu()
+            self._host_halo = (torch.empty(P), torch.empty(P))
+            hp, hn = self._host_halo
         ops_ = [
             dist.P2POp(dist.isend, last, self.next_rank, self.group, tag=0),
-            dist.P2POp(dist.irecv, self.halo_prev[:P], self.prev_rank, self.group, tag=0),
+            dist.P2POp(dist.irecv, hp, self.prev_rank, self.group, tag=0),
             dist.P2POp(dist.isend, first, self.prev_rank, self.group, tag=1),
-            dist.P2POp(dist.irecv, self.halo_next[:P], self.next_rank, self.group, tag=1),
+            dist.P2POp(dist.irecv, hn, self.next_rank, self.group, tag=1),
         ]
         return dist.batch_isend_irecv(ops_)
+
+    def _finish_exchange(self, reqs) -> None:
+        for r in reqs:
+            r.wait()
+        if self._staged():
+            self.halo_prev[: self.P].copy_(self._host_halo[0])
+            self.halo_next[: self.P].copy_(self._host_halo[1])
 
     def step(self, x: Optional[torch.Tensor] = None, y: Optional[torch.Tensor] = None) -> None:
         """One Jacobi round Y = W X on the local block (then swap if using own buffers)."""
@@ -105,8 +121,7 @@ class ShardedRing:
                           halo_next=x[n - 1], P=P, n_rows=n - 2)
                 if ev:
                     ev[1].record()
-            for r in reqs:
-                r.wait()
+            self._finish_exchange(reqs)
             # boundary rows 0 and n-1
             self._mix(x[0:1], y[0:1], self.w_prev[0:1], self.w_next[0:1], halo_prev=self.halo_prev,
                       halo_next=x[1], P=P, n_rows=1)
@@ -132,7 +147,12 @@ def global_mean(local_rows: torch.Tensor, local_order: Sequence[int], m_total: i
     else:
         out.zero_()
     if dist.is_initialized() and dist.get_world_size(group) > 1:
-        dist.all_reduce(out, op=dist.ReduceOp.SUM, group=group)
+        if out.device.type == "cuda" and dist.get_backend(group) == "gloo":
+            host = out.cpu()
+            dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)
+            out.copy_(host)
+        else:
+            dist.all_reduce(out, op=dist.ReduceOp.SUM, group=group)
     zero = torch.empty(0, dtype=torch.int32, device=device)
     return ordered_sum(None, zero, acc_in=out, out=out, scale=float(m_total), P=P)
 
