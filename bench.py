@@ -57,11 +57,11 @@ def parse():
 
 
 def ring_weights(n: int):
-    """W = communication_graph('circle', 'stochastic', n) after manual_seed(2028)."""
+    """W = communication_graph('circle', 'stochastic', n) after manual_seed(2028), built
+    sparse (bit-identical, tests/test_graph_host.py) so 8 ranks don't each hold a dense W."""
     from dolhip import graph as G
     torch.manual_seed(2028)
-    W = G.communication_graph("circle", "stochastic", n)[0]
-    rw = G.csr_from_dense(W).ring_weights()
+    rw = G.communication_csr("circle", "stochastic", n)[0].ring_weights()  # = csr_from_dense(communication_graph(...))
     assert rw is not None
     return rw
 

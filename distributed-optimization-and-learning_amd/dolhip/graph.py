@@ -112,6 +112,67 @@ def communication_graph(topology: str, mode: str, n: int, sinkhorn_max_iters: in
     return graphs
 
 
+def communication_csr(topology: str, mode: str, n: int, **kw) -> List["CSR"]:
+    """communication_graph(...) as CSRs (Neighbors' selection applied),
+    without materialising a dense N x N matrix per time step.
+
+    circle / dynamic with mode 'stochastic' or a raw mode are built straight
+    from the ONE torch.rand(n, n) draw the reference makes (so the global RNG
+    advances identically): every column of R o A has at most two nonzeros, so
+    its sum — and therefore every W entry — is the same whatever order torch's
+    column reduction uses.  The reference's 'dynamic' list would be n dense
+    n x n matrices (2 TB at n = 8192); here it is n CSRs of 2 entries.
+    Other topologies/modes go through the dense construction."""
+    topo = "compelete" if topology == "complete" else topology
+    weighted = mode == "stochastic"
+    raw = mode not in ("stochastic", "double_stochastic")
+    if topo not in ("circle", "dynamic") or not (weighted or raw):
+        return [csr_from_dense(g) for g in communication_graph(topology, mode, n, **kw)]
+    R = torch.rand(n, n).numpy() if weighted else None
+
+    def build(edges):
+        # edges: undirected pairs (a, b); A[a][b] = A[b][a] = 1
+        A = {}
+        for a, b in edges:
+            A[(a, b)] = 1.0
+            A[(b, a)] = 1.0
+        if raw:
+            vals = {(i, j): np.float32(1.0) for (i, j) in A}
+        else:
+            colsum = {}
+            for (i, j) in A:  # G[i][j] = R[i][j]; W[j][i] = G[i][j] / colsum_j
+                colsum[j] = np.float32(colsum.get(j, np.float32(0.0)) + np.float32(R[i, j]))
+            with np.errstate(invalid="ignore", divide="ignore"):
+                vals = {(j, i): np.float32(np.float32(R[i, j]) / colsum[j]) for (i, j) in A}
+        rows = {}
+        for (i, j), v in vals.items():
+            if v > 0:  # Neighbors keeps W[i][j] > 0 (NaN and 0 drop out)
+                rows.setdefault(i, []).append((j, v))
+        rowptr = np.zeros(n + 1, np.int64)
+        cols, vv = [], []
+        for i in range(n):
+            for j, v in sorted(rows.get(i, [])):
+                cols.append(j)
+                vv.append(v)
+            rowptr[i + 1] = len(cols)
+        return CSR(n, n, rowptr.astype(np.int32), np.asarray(cols, np.int32), np.asarray(vv, np.float32))
+
+    if topo == "circle":
+        if n == 1:
+            return [csr_from_dense(g) for g in _graphs_from_rand(topology, mode, n, R)]
+        return [build([(i, (i + 1) % n) for i in range(n)])]
+    return [build([(t, (t + 1) % n)]) for t in range(n)]
+
+
+def _graphs_from_rand(topology, mode, n, R):
+    """Dense fallback that reuses an already drawn R (keeps the RNG stream)."""
+    graphs = list(adjacency(topology, n))
+    if mode == "stochastic":
+        rand = torch.from_numpy(R)
+        return [_column_stochastic_T(rand, a) for a in graphs]
+    return graphs
+
+
 @dataclass
 class CSR:
     """Host CSR of a mixing matrix (int32 rowptr/col, fp32 val)."""

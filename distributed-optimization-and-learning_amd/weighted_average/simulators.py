@@ -50,19 +50,28 @@ class Simulator(object):
     def select_global_model(self, model, device):
         return select_model(model, device if device is not None else "cuda")
 
+    SPARSE_ABOVE = 2048  # agents; above this W[t] is kept as CSR only
+
     def communication_graph(self, topology, mode, n):
-        """W[t] exactly as DIST/simulators.py:40-86 (bounded Sinkhorn)."""
+        """W[t] exactly as DIST/simulators.py:40-86 (bounded Sinkhorn).  Dense
+        matrices like the reference for small n; for n > SPARSE_ABOVE (or
+        args.sparse_graphs) the same W as CSRs (dolhip.graph.communication_csr),
+        e.g. 'dynamic' at 8192 agents is 8192 two-entry CSRs, not 2 TB."""
         kw = {}
         if self.args.sinkhorn_max_iters is not None:
             kw["sinkhorn_max_iters"] = self.args.sinkhorn_max_iters
         if self.args.sinkhorn_tol is not None:
             kw["sinkhorn_tol"] = self.args.sinkhorn_tol
+        sparse = self.args.sparse_graphs if self.args.sparse_graphs is not None else n > self.SPARSE_ABOVE
+        if sparse:
+            return G.communication_csr(topology, mode, n, **kw)
         return G.communication_graph(topology, mode, n, verbose=bool(self.args.verbose), **kw)
 
     def plan(self, t: int) -> G.MixingPlan:
         p = self._plans.get(t)
         if p is None:
-            p = G.MixingPlan.from_graph(self.adjacent_matrix[t], self.device)
+            g = self.adjacent_matrix[t]
+            p = G.MixingPlan(g, self.device) if isinstance(g, G.CSR) else G.MixingPlan.from_graph(g, self.device)
             self._plans[t] = p
         return p
 
@@ -76,12 +85,19 @@ class Simulator(object):
     def Neighbors(self, i, graph):
         """[(W[i][j], state_dict of agent j)] for j ascending with W[i][j] > 0
         (DIST/simulators.py:91-97), read from the CSR form of the graph."""
+        if isinstance(graph, G.CSR):
+            s, e = graph.rowptr[i], graph.rowptr[i + 1]
+            return [(torch.tensor(graph.val[k]), self.clients[int(graph.col[k])].model.state_dict())
+                    for k in range(s, e)]
         csr = G.csr_from_dense(graph)
         s, e = csr.rowptr[i], csr.rowptr[i + 1]
         return [(graph[i][int(j)], self.clients[int(j)].model.state_dict()) for j in csr.col[s:e]]
 
     def _print_graph(self, graph):
         print("\n | Communication Graph")
+        if isinstance(graph, G.CSR):
+            print(f"   [{graph.n_rows} x {graph.n_cols} mixing matrix, {graph.nnz} nonzeros (CSR)]\n")
+            return
         rows = graph.numpy() if isinstance(graph, torch.Tensor) else graph
         if len(rows) <= 32:
             for row in rows:

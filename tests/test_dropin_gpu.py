@@ -170,3 +170,18 @@ def test_bank_checkpoint_roundtrip(gpu, tmp_path):
     b = AgentBank(5, [("w", (3, 7)), ("b", (11,))], gpu)
     b.load(p)
     assert torch.equal(a.rows(), b.rows()) and torch.equal(a.rows("mom"), b.rows("mom"))
+
+
+def test_sparse_graphs_simulator_matches_dense(gpu):
+    """args.sparse_graphs keeps W[t] as CSR; the mixing is identical."""
+    m = load_project("weighted_average", ["simulators", "utils"])
+    outs = []
+    for sparse in (False, True):
+        args = _small_dist_args(m["utils"], topology="dynamic", sparse_graphs=sparse, num_users=6)
+        sim = m["simulators"].DecFedAvg(args)
+        assert isinstance(sim.adjacent_matrix[0], m["simulators"].G.CSR) == sparse
+        for t in range(3):
+            sim.mix(t)
+        outs.append(sim.bank.rows().cpu().numpy())
+        assert len(sim.Neighbors(0, sim.adjacent_matrix[0])) == 1
+    assert oracle.bits_equal(outs[0], outs[1])

@@ -123,3 +123,30 @@ def test_shard_bounds_partition(n, world):
         assert a1 == b0
     sizes = [hi - lo for lo, hi in b]
     assert max(sizes) - min(sizes) <= 1
+
+
+@pytest.mark.parametrize("topo,mode,n", [("circle", "stochastic", n) for n in (1, 2, 3, 5, 6, 16, 64, 300)] +
+                         [("dynamic", "stochastic", n) for n in (2, 3, 6, 17)] +
+                         [("circle", "none", 6), ("dynamic", "none", 5), ("star", "stochastic", 6),
+                          ("compelete", "stochastic", 5), ("circle", "double_stochastic", 6)])
+def test_communication_csr_equals_dense_path(topo, mode, n):
+    """The sparse builder gives bit-identical CSRs and consumes the same RNG."""
+    torch.manual_seed(2028)
+    dense = [G.csr_from_dense(g) for g in G.communication_graph(topo, mode, n)]
+    after_dense = torch.rand(3)
+    torch.manual_seed(2028)
+    sparse = G.communication_csr(topo, mode, n)
+    assert torch.equal(torch.rand(3), after_dense)
+    assert len(dense) == len(sparse)
+    for a, b in zip(dense, sparse):
+        assert np.array_equal(a.rowptr, b.rowptr) and np.array_equal(a.col, b.col)
+        assert a.val.tobytes() == b.val.tobytes()
+
+
+def test_dynamic_8192_is_sparse_and_fast():
+    import time
+    torch.manual_seed(2028)
+    t = time.time()
+    gs = G.communication_csr("dynamic", "stochastic", 8192)
+    assert len(gs) == 8192 and all(g.nnz == 2 for g in gs[:10])
+    assert time.time() - t < 60
