@@ -21,12 +21,12 @@
 #include <type_traits>
 
 #include "../../include/dol_hip.h"
-
-namespace {
+#include "dol_common.h"
 
 // ----------------------------------------------------------------------------
-// error plumbing
+// error plumbing (shared with the other translation units via dol_common.h)
 // ----------------------------------------------------------------------------
+namespace dol {
 thread_local char g_err[512] = "";
 
 int fail(int code, const char* fmt, ...) {
@@ -45,6 +45,12 @@ int check_launch(const char* what) {
   g_err[0] = '\0';
   return DOL_OK;
 }
+}  // namespace dol
+
+namespace {
+using dol::check_launch;
+using dol::fail;
+using dol::g_err;
 
 constexpr int kThreads = 256;            // 4 waves of 64
 constexpr int64_t kMaxBlocks = int64_t(1) << 24;

@@ -1,0 +1,551 @@
+// mlp_step.hip — one fused local step of N independent per-agent MLPs on fp32 MFMA.
+//
+// Each agent k owns nn.Sequential(Linear(d, h), ReLU(), Linear(h, c)) whose
+// parameters are row k of the stacked bank (state_dict order: W1 [h,d], b1 [h],
+// W2 [c,h], b2 [c]).  One workgroup (4 waves) runs one agent's whole step —
+// the body of the reference's per-agent local_update loop (DIST/clients.py:
+// 34-59: forward, CrossEntropyLoss, backward, optimizer.step(); with the
+// FedProx / FedADMM gradient terms of DEC/clients.py:101-139) — in ONE pass:
+//
+//   F1  Z1^T = W1 X^T          v_mfma_f32_32x32x2_f32, K = d, W1 / X streamed as 64 B/lane
+//       H = relu(Z1 + b1)      -> LDS  Hs[b][h]
+//   F2  Z2 = H W2^T + b2       VALU (c is tiny), W2 staged in LDS
+//   CE  dZ2 = (softmax(Z2) - onehot(y)) / B, loss = mean_b(lse - Z2[y])
+//   B2  dW2 = dZ2^T H, db2, dZ1 = (dZ2 W2) * [H > 0], db1     VALU, LDS
+//   B1  dW1 = dZ1^T X          MFMA, K = B; each 32x32 tile of dW1 is consumed
+//                              in registers by the fused update of the W1 tile.
+//
+// Two launches: mlp_fwd_kernel (one workgroup per agent: F1 .. B2 and the
+// updates of b1, W2, b2; dZ1 goes to a B x h workspace per agent) and
+// mlp_dw1_kernel (one short-lived workgroup per agent x 32-column tile of W1:
+// B1 + the W1 update).  W1 / momentum dominate the bytes and stream through
+// the second kernel at full occupancy; a single-kernel version that walked
+// each agent's 25 W1 tiles inside the per-agent workgroup ran 2.4x slower
+// (one HBM round trip per tile, 2-3 waves per SIMD; tools/mlp_phase.hip).
+//   update (every parameter, as dol_prox_admm_sgd_f32):
+//       g' = g [+ (alpha +) rho*(w - theta)];  buf = mom*buf + g' (buf = g' on the
+//       first step);  w = fma(-lr, buf, w)
+//
+// The per-agent gradients never touch HBM (unless write_grad asks for them),
+// so a step moves W1 in + out, the momentum buffer in + out and X in, instead
+// of the unfused path's extra gradient write + read.  GEMM numerics: fp32
+// MFMA = a k-ordered f32 fma chain; the reference's torch CPU GEMMs use a
+// different blocking, so this path is tolerance-checked (tests/test_mlp_gpu.py),
+// not bit-exact.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+#include <type_traits>
+
+#include "../../include/dol_hip.h"
+#include "dol_common.h"
+
+namespace {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kWaves = 4;
+constexpr int kThreads = 64 * kWaves;
+constexpr int kMaxB = 64, kMaxH = 256, kMaxC = 32;
+
+struct MlpArgs {
+  float* W; int64_t ldw;         // parameter rows
+  float* G; int64_t ldg;         // gradient rows (written when write_grad), nullable
+  float* M; int64_t ldm;         // momentum rows, nullable when mode == 0
+  const float* theta;            // [P] global model (FedProx / FedADMM), nullable
+  const float* A; int64_t lda;   // ADMM duals, nullable
+  const float* X; int64_t ldxa, ldxb;  // batch: agent stride, sample stride (floats)
+  const int64_t* Y; int64_t ldya;      // labels [n][B]
+  float* loss;                   // [n] mean CE per agent, nullable
+  int B, d, h, c;
+  float neg_lr, mom, rho;
+  int mode;                      // 0 plain SGD, 1 momentum first step, 2 momentum
+  int update;                    // 0: gradients only (forward_backward)
+#ifdef DOL_MLP_TRACE
+  long long* trace;              // tools/mlp_phase.hip: per-agent phase timestamps
+#endif
+};
+
+#ifdef DOL_MLP_TRACE
+#define DOL_TRACE(i) \
+  if (threadIdx.x == 0 && a.trace) a.trace[int64_t(blockIdx.x) * 8 + (i)] = wall_clock64();
+#else
+#define DOL_TRACE(i)
+#endif
+
+// Gradient term + optimizer update of N parameters (same rounding sequence as
+// prox_sgd_lane in dol_hip.hip).  All loads of the batch are issued before any
+// store (load() first, e.g. ahead of the MFMAs that produce the gradients, then
+// commit()): the rows are plain float*, so a load-update-store per element
+// would serialise one memory round trip per element.  Loads are unconditional
+// from always-valid addresses (idx(i) stays in the row even for dead lanes):
+// a predicated load compiles to a branch + s_waitcnt vmcnt(0) per element.
+// UPD: 0 = gradients only, 1 = SGD, 2 = momentum first step, 3 = momentum.
+// TH / AL: the FedProx / FedADMM terms are compiled in (theta / alpha non-null).
+template <int N, int UPD, bool TH, bool AL>
+struct ParamBatch {
+  float w[N], m[N], th[N], al[N];
+
+  // idx(i): row offset of element i (valid even when !ok(i)); ok(i): element i is live
+  template <class Idx>
+  __device__ __forceinline__ void load(const MlpArgs& a, const float* wrow, const float* mrow, const float* arow,
+                                       Idx idx) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      if constexpr (UPD > 0 || TH) w[i] = wrow[idx(i)];
+      if constexpr (UPD == 3) m[i] = mrow[idx(i)];
+      if constexpr (TH) th[i] = a.theta[idx(i)];
+      if constexpr (AL) al[i] = arow[idx(i)];
+    }
+  }
+
+  // g[i]: raw loss gradient of element i
+  template <class Idx, class Ok>
+  __device__ __forceinline__ void commit(const MlpArgs& a, float* wrow, float* grow, float* mrow, const float (&g)[N],
+                                         Idx idx, Ok ok) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      float gg = g[i];
+      if constexpr (TH) {
+        float t = a.rho * (w[i] - th[i]);
+        if constexpr (AL) t = al[i] + t;
+        gg = gg + t;
+      }
+      float dd = gg;
+      if constexpr (UPD == 2) {
+        m[i] = gg;
+      } else if constexpr (UPD == 3) {
+        m[i] = m[i] * a.mom + gg;
+        dd = m[i];
+      }
+      if (!ok(i)) continue;
+      if (grow) grow[idx(i)] = gg;
+      if constexpr (UPD > 0) __builtin_nontemporal_store(__builtin_fmaf(a.neg_lr, dd, w[i]), wrow + idx(i));
+      if constexpr (UPD >= 2) __builtin_nontemporal_store(m[i], mrow + idx(i));
+    }
+  }
+};
+
+#define DOL_GPTR(p) ((const __attribute__((address_space(1))) void*)(p))
+#define DOL_LPTR(p) ((__attribute__((address_space(3))) void*)(p))
+
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n (the immediate must be a constant)
+__device__ __forceinline__ void wait_vmcnt(int n) {
+  switch (n) {
+#define DOL_VMC(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
+    DOL_VMC(0) DOL_VMC(1) DOL_VMC(2) DOL_VMC(3) DOL_VMC(4) DOL_VMC(5) DOL_VMC(6) DOL_VMC(7)
+    DOL_VMC(8) DOL_VMC(9) DOL_VMC(10) DOL_VMC(11) DOL_VMC(12) DOL_VMC(13) DOL_VMC(14) DOL_VMC(15)
+#undef DOL_VMC
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+constexpr int kStages = 3;  // F1 LDS-DMA pipeline depth (two chunks in flight during the MFMAs)
+
+// LDS layout of mlp_fwd_kernel (floats): [ union: F1 staging | Hs, W2s, Zs ] [ b1s, b2s, ls ] [ ys ]
+__host__ __device__ inline int64_t fwd_union_floats(int B, int h, int c) {
+  const int64_t Bp = 32 * ((B + 31) / 32);
+  const int64_t staging = int64_t(kStages) * (h + Bp) * 32;
+  const int64_t post = int64_t(B) * (h + 4) + int64_t(c) * (h + 4) + int64_t(B) * c;
+  return staging > post ? staging : post;
+}
+
+// Per-agent part: forward, CE, backward down to dZ1 (-> ws[agent][b][h]),
+// updates of b1, W2, b2.
+// F1 streams W1 and X through LDS with global_load_lds (LDS-DMA): each
+// 32-wide k chunk of the h + Bp rows lands as 128-B rows whose 16-B pieces are
+// XOR-swizzled by row (piece p of row r at slot p ^ (r & 7)), three stages
+// deep; a row-contiguous load touches 8 lines per instruction where reading
+// the MFMA fragments straight from HBM touched 64 (2.3 TB/s effective).
+// NT = accumulator tiles per wave: 1 when h * ceil(B/32) <= 128, else 4.
+template <int NT, int UPD, bool TH, bool AL>
+__global__ __launch_bounds__(kThreads) void mlp_fwd_kernel(MlpArgs a, float* __restrict__ ws) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int B = a.B, d = a.d, h = a.h, c = a.c;
+  const int hp = h + 4;  // padded LDS rows: 16-B aligned, rows 4 banks apart
+  float* Hs = lds;                   // [B][hp]  H, later dZ1   (after F1)
+  float* W2s = Hs + B * hp;          // [c][hp]                 (after F1)
+  float* Zs = W2s + c * hp;          // [B][c]   Z2, later dZ2
+  float* b1s = lds + fwd_union_floats(B, h, c);  // [h]
+  float* b2s = b1s + h;              // [c]
+  float* ls = b2s + c;               // [B] per-sample loss
+  int* ys = reinterpret_cast<int*>(ls + B);  // [B]
+
+  const int agent = blockIdx.x;
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int li = lane & 31, hh = lane >> 5;
+  float* wrow = a.W + int64_t(agent) * a.ldw;
+  float* grow = a.G ? a.G + int64_t(agent) * a.ldg : nullptr;
+  float* mrow = a.M ? a.M + int64_t(agent) * a.ldm : nullptr;
+  const float* arow = a.A ? a.A + int64_t(agent) * a.lda : nullptr;
+  const float* xa = a.X + int64_t(agent) * a.ldxa;
+  const int64_t oW1 = 0, ob1 = int64_t(h) * d, oW2 = ob1 + h, ob2 = oW2 + int64_t(c) * h;
+
+  DOL_TRACE(0)
+  // update operands of W2 (first 8 * 256 entries), b1 and b2 go out now, so
+  // their round trips overlap F1 instead of serialising the B2 phase
+  auto ok_w2 = [&](int i) { return i * kThreads + t < c * h; };
+  auto idx_w2 = [&](int i) { return oW2 + (ok_w2(i) ? i * kThreads + t : 0); };
+  auto ok_b1 = [&](int) { return t < h; };
+  auto idx_b1 = [&](int) { return ob1 + (t < h ? t : 0); };
+  auto ok_b2 = [&](int) { return t < c; };
+  auto idx_b2 = [&](int) { return ob2 + (t < c ? t : 0); };
+  ParamBatch<8, UPD, TH, AL> pw2;
+  ParamBatch<1, UPD, TH, AL> pb1, pb2;
+  pw2.load(a, wrow, mrow, arow, idx_w2);
+  pb1.load(a, wrow, mrow, arow, idx_b1);
+  pb2.load(a, wrow, mrow, arow, idx_b2);
+  for (int i = t; i < h; i += kThreads) b1s[i] = wrow[ob1 + i];
+  if (t < c) b2s[t] = wrow[ob2 + t];
+  if (t < B) ys[t] = static_cast<int>(a.Y[int64_t(agent) * a.ldya + t]);
+  __syncthreads();
+
+  // ---- F1: Z1^T tiles (32 h x 32 b) on MFMA, K = d in chunks of 32
+  const int nht = h / 32, nbt = (B + 31) / 32;
+  const int Bp = 32 * nbt, rows = h + Bp;  // staged rows per chunk (W1 rows, then X rows)
+  const int ipw = rows / 32;               // DMA instructions per wave per chunk (8 rows each)
+  const int nk = (d + 31) / 32;
+  float* stg = lds;
+  auto issue = [&](int kc) {
+    float* st = stg + (kc % kStages) * rows * 32;
+    for (int i = 0; i < ipw; ++i) {
+      const int ins = wave + kWaves * i;
+      const int r = 8 * ins + (lane >> 3);
+      const int ch = (lane & 7) ^ (lane >> 3);
+      int k = kc * 32 + 4 * ch;
+      k = k < d ? k : 0;  // clamped in-bounds; zeroed after landing
+      const float* src = (r < h) ? wrow + oW1 + int64_t(r) * d + k
+                                 : xa + int64_t(min(r - h, B - 1)) * a.ldxb + k;
+      __builtin_amdgcn_global_load_lds(DOL_GPTR(src), DOL_LPTR(st + ins * 256), 16, 0, 0);
+    }
+  };
+  f32x16 acc[NT];
+#pragma unroll
+  for (int u = 0; u < NT; ++u)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[u][r] = 0.f;
+  issue(0);
+  if (nk > 1) issue(1);
+  for (int kc = 0; kc < nk; ++kc) {
+    wait_vmcnt(kc + 1 < nk ? ipw : 0);  // chunk kc landed (kc + 1 may still fly)
+    __builtin_amdgcn_s_barrier();       // ... for every wave; and stage (kc + 2) % 3 is free
+    const float* st = stg + (kc % kStages) * rows * 32;
+    if (kc == nk - 1 && (d & 31)) {     // zero the clamped k >= d pieces of the tail chunk
+      for (int i = 0; i < ipw; ++i) {
+        const int ins = wave + kWaves * i;
+        if (kc * 32 + 4 * ((lane & 7) ^ (lane >> 3)) >= d)
+          *reinterpret_cast<f4*>(const_cast<float*>(st) + ins * 256 + lane * 4) = f4{0.f, 0.f, 0.f, 0.f};
+      }
+      __syncthreads();
+    }
+    if (kc + 2 < nk) issue(kc + 2);
+#pragma unroll
+    for (int u = 0; u < NT; ++u) {
+      const int tile = wave + kWaves * u;
+      if (tile < nht * nbt) {
+        const int ht = tile % nht, bt = tile / nht;
+        const float* ar = st + (32 * ht + li) * 32;
+        const float* xr = st + (h + 32 * bt + li) * 32;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int pos = ((4 * hh + j) ^ (li & 7)) * 4;
+          const f4 av = *reinterpret_cast<const f4*>(ar + pos);
+          const f4 xv = *reinterpret_cast<const f4*>(xr + pos);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc[u] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[q], xv[q], acc[u], 0, 0, 0);
+        }
+      }
+    }
+  }
+  __syncthreads();  // staging is dead: Hs / W2s / Zs reuse it
+  // C/D map: col (b) = lane & 31, row (h) = (r&3) + 8*(r>>2) + 4*(lane>>5)
+#pragma unroll
+  for (int u = 0; u < NT; ++u) {
+    const int tile = wave + kWaves * u;
+    if (tile < nht * nbt) {
+      const int ht = tile % nht, bt = tile / nht;
+      const int brow = 32 * bt + li;
+      if (brow < B) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int hr = 32 * ht + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          const float z = acc[u][r] + b1s[hr];
+          Hs[brow * hp + hr] = (z > 0.0f || z != z) ? z : 0.0f;  // relu, NaN propagates like torch
+        }
+      }
+    }
+  }
+  for (int i = t; i < c * h; i += kThreads) W2s[(i / h) * hp + i % h] = wrow[oW2 + i];
+  __syncthreads();
+
+  DOL_TRACE(1)
+  // ---- F2: Z2 = H W2^T + b2
+  for (int o = t; o < B * c; o += kThreads) {
+    const int b = o / c, j = o % c;
+    float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;  // h % 32 == 0
+    for (int k = 0; k < h; k += 4) {
+      const f4 hv = *reinterpret_cast<const f4*>(Hs + b * hp + k);
+      const f4 wv = *reinterpret_cast<const f4*>(W2s + j * hp + k);
+      s0 = s0 + hv.x * wv.x;
+      s1 = s1 + hv.y * wv.y;
+      s2 = s2 + hv.z * wv.z;
+      s3 = s3 + hv.w * wv.w;
+    }
+    Zs[o] = ((s0 + s1) + (s2 + s3)) + b2s[j];
+  }
+  __syncthreads();
+
+  // ---- CE: log-softmax per sample, dZ2 = (p - onehot) / B
+  if (t < B) {
+    float* z = Zs + t * c;
+    float m = z[0];
+    for (int j = 1; j < c; ++j) m = fmaxf(m, z[j]);
+    float s = 0.0f;
+    for (int j = 0; j < c; ++j) s = s + expf(z[j] - m);
+    const float lse = m + logf(s);
+    const int y = ys[t];
+    const bool yok = y >= 0 && y < c;
+    ls[t] = yok ? lse - z[yok ? y : 0] : __builtin_nanf("");
+    const float invB = 1.0f / static_cast<float>(B);
+    for (int j = 0; j < c; ++j) z[j] = (expf(z[j] - lse) - (j == y ? 1.0f : 0.0f)) * invB;
+  }
+  __syncthreads();
+  if (t == 0 && a.loss) {
+    float s = 0.0f;
+    for (int b = 0; b < B; ++b) s = s + ls[b];
+    a.loss[agent] = s / static_cast<float>(B);
+  }
+
+  DOL_TRACE(2)
+  // ---- B2a: dW2 = dZ2^T H, db2 = sum_b dZ2 (and their parameter updates; the
+  // forward already used W2 / b2 from LDS)
+  for (int o0 = 0; o0 < c * h; o0 += 8 * kThreads) {
+    ParamBatch<8, UPD, TH, AL> pb;
+    float g[8];
+    auto ok = [&](int i) { return o0 + i * kThreads + t < c * h; };
+    auto idx = [&](int i) { return oW2 + (ok(i) ? o0 + i * kThreads + t : 0); };
+    if (o0 > 0) pb.load(a, wrow, mrow, arow, idx);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int o = ok(i) ? o0 + i * kThreads + t : 0;
+      const int j = o / h, k = o % h;
+      float s = 0.0f;
+      for (int b = 0; b < B; ++b) s = s + Zs[b * c + j] * Hs[b * hp + k];
+      g[i] = s;
+    }
+    if (o0 == 0) pw2.commit(a, wrow, grow, mrow, g, idx, ok);
+    else pb.commit(a, wrow, grow, mrow, g, idx, ok);
+  }
+  if (t < 64) {  // db2 (c <= 32 lanes of wave 0)
+    float g[1];
+    const int j = t < c ? t : 0;
+    float s = 0.0f;
+    for (int b = 0; b < B; ++b) s = s + Zs[b * c + j];
+    g[0] = s;
+    pb2.commit(a, wrow, grow, mrow, g, idx_b2, ok_b2);
+  }
+  __syncthreads();
+
+  // ---- B2b: dZ1 = (dZ2 W2) * [H > 0], in place over H
+#pragma unroll 4
+  for (int o = t; o < B * h; o += kThreads) {
+    const int b = o / h, k = o % h;
+    float s = 0.0f;
+    for (int j = 0; j < c; ++j) s = s + Zs[b * c + j] * W2s[j * hp + k];
+    float* hv = Hs + b * hp + k;
+    *hv = (*hv > 0.0f) ? s : 0.0f;
+  }
+  __syncthreads();
+
+  // ---- db1 (h <= kThreads)
+  {
+    float g[1];
+    float s = 0.0f;
+    if (t < h)
+      for (int b = 0; b < B; ++b) s = s + Hs[b * hp + t];
+    g[0] = s;
+    pb1.commit(a, wrow, grow, mrow, g, idx_b1, ok_b1);
+  }
+
+  // dZ1 for the W1 tiles of mlp_dw1_kernel
+  float* wsa = ws + int64_t(agent) * B * h;
+  for (int o = t; o < B * h; o += kThreads) wsa[o] = Hs[(o / h) * hp + (o % h)];
+  DOL_TRACE(3)
+}
+
+// B1 + W1 update: block agent * ndt + dt owns columns [32 dt, 32 dt + 32) of W1
+// for all h rows; wave w takes h-tiles w, w + 4, ...  A = dZ1^T from the
+// workspace (L2), B = X[:, cols].  Memory goes through wave-uniform buffer
+// descriptors: one 32-bit lane offset per tile, the row step of each of the
+// 16 accumulator rows in the SGPR soffset, dead lanes pointed out of range
+// (loads return 0, stores are dropped), and every load of the tile issued
+// before the MFMA chain (sched_barrier) so the W1 / momentum reads overlap it.
+// KS = MFMA k-steps (2 samples each): 16 for B <= 32, 32 for B <= 64.
+using rsrc_t = __amdgpu_buffer_rsrc_t;
+constexpr uint32_t kOOB = 0x80000000u;  // any lane offset >= every buffer's size
+
+__device__ __forceinline__ rsrc_t make_rsrc(const float* p, int64_t nbytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), 0, static_cast<int>(nbytes), 0x00020000);
+}
+__device__ __forceinline__ float bload(rsrc_t r, uint32_t voff, uint32_t soff) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, static_cast<int>(voff), static_cast<int>(soff), 0));
+}
+__device__ __forceinline__ void bstore_nt(rsrc_t r, uint32_t voff, uint32_t soff, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, static_cast<int>(voff), static_cast<int>(soff), 2);
+}
+
+template <int KS, int UPD, bool TH, bool AL>
+__global__ __launch_bounds__(kThreads) void mlp_dw1_kernel(MlpArgs a, const float* __restrict__ ws) {
+  const int B = a.B, d = a.d, h = a.h, c = a.c;
+  const int ndt = (d + 31) / 32;
+  const int dt = static_cast<int>(blockIdx.x % ndt), agent = static_cast<int>(blockIdx.x / ndt);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int li = lane & 31, hh = lane >> 5;
+  const int64_t P = int64_t(h) * d + h + int64_t(c) * h + c;
+  const rsrc_t rW = make_rsrc(a.W + int64_t(agent) * a.ldw, P * 4);
+  const rsrc_t rM = make_rsrc(UPD == 3 || UPD == 2 ? a.M + int64_t(agent) * a.ldm : a.W, P * 4);
+  const rsrc_t rG = make_rsrc(a.G ? a.G + int64_t(agent) * a.ldg : a.W, a.G ? P * 4 : 0);
+  const rsrc_t rT = make_rsrc(TH ? a.theta : a.W, TH ? P * 4 : 0);
+  const rsrc_t rA = make_rsrc(AL ? a.A + int64_t(agent) * a.lda : a.W, AL ? P * 4 : 0);
+  const rsrc_t rX = make_rsrc(a.X + int64_t(agent) * a.ldxa, (int64_t(B - 1) * a.ldxb + d) * 4);
+  const rsrc_t rZ = make_rsrc(ws + int64_t(agent) * B * h, int64_t(B) * h * 4);
+  const int col = 32 * dt + li;
+  const bool cok = col < d;
+  float xv[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int b = 2 * s + hh;
+    xv[s] = bload(rX, (b < B && cok) ? uint32_t((b * a.ldxb + col) * 4) : kOOB, 0);
+  }
+  for (int ht = wave; ht < h / 32; ht += kWaves) {
+    float av[KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int b = 2 * s + hh;
+      av[s] = bload(rZ, b < B ? uint32_t((b * h + 32 * ht + li) * 4) : kOOB, 0);
+    }
+    const uint32_t pv = cok ? uint32_t(((32 * ht + 4 * hh) * d + col) * 4) : kOOB;
+    auto so = [&](int r) { return uint32_t(((r & 3) + 8 * (r >> 2)) * d * 4); };
+    float w[16], m[16], th[16], al[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      if constexpr (UPD > 0 || TH) w[r] = bload(rW, pv, so(r));
+      if constexpr (UPD == 3) m[r] = bload(rM, pv, so(r));
+      if constexpr (TH) th[r] = bload(rT, pv, so(r));
+      if constexpr (AL) al[r] = bload(rA, pv, so(r));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], xv[s], acc, 0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float gg = acc[r];
+      if constexpr (TH) {
+        float t = a.rho * (w[r] - th[r]);
+        if constexpr (AL) t = al[r] + t;
+        gg = gg + t;
+      }
+      float dd = gg;
+      if constexpr (UPD == 2) {
+        m[r] = gg;
+      } else if constexpr (UPD == 3) {
+        m[r] = m[r] * a.mom + gg;
+        dd = m[r];
+      }
+      if (a.G) bstore_nt(rG, pv, so(r), gg);
+      if constexpr (UPD > 0) bstore_nt(rW, pv, so(r), __builtin_fmaf(a.neg_lr, dd, w[r]));
+      if constexpr (UPD >= 2) bstore_nt(rM, pv, so(r), m[r]);
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int64_t dol_mlp_step_workspace_bytes(int32_t n_agents, int32_t B, int32_t h) {
+  if (n_agents <= 0 || B <= 0 || h <= 0) return 0;
+  return int64_t(n_agents) * B * h * int64_t(sizeof(float));
+}
+
+extern "C" int64_t dol_mlp_step_lds_bytes(int32_t B, int32_t h, int32_t c) {
+  return sizeof(float) * (fwd_union_floats(B, h, c) + h + c + B) + sizeof(int) * int64_t(B);
+}
+
+extern "C" int dol_mlp_step_f32(float* w, int64_t ldw, float* grad, int64_t ldg, float* mom, int64_t ldm,
+                                const float* theta, const float* alpha, int64_t lda, const float* X,
+                                int64_t ldx_agent, int64_t ldx_row, const int64_t* labels, int64_t ldy_agent,
+                                float* loss, int32_t n_agents, int32_t B, int32_t d, int32_t h, int32_t c,
+                                float lr, float momentum, float rho, int first_step, int update,
+                                void* work, hipStream_t s) {
+  using dol::fail;
+  if (n_agents < 0) return fail(DOL_EINVAL, "dol_mlp_step_f32: negative agent count");
+  if (n_agents == 0) { dol::g_err[0] = '\0'; return DOL_OK; }
+  if (B < 1 || B > kMaxB) return fail(DOL_EINVAL, "dol_mlp_step_f32: batch %d outside [1, %d]", B, kMaxB);
+  if (h < 32 || h > kMaxH || h % 32) return fail(DOL_EINVAL, "dol_mlp_step_f32: hidden %d must be a multiple of 32 in [32, %d]", h, kMaxH);
+  if (c < 1 || c > kMaxC) return fail(DOL_EINVAL, "dol_mlp_step_f32: classes %d outside [1, %d]", c, kMaxC);
+  if (d < 4 || d % 4) return fail(DOL_EINVAL, "dol_mlp_step_f32: input dim %d must be a positive multiple of 4", d);
+  if (!w || !X || !labels || !work) return fail(DOL_EINVAL, "dol_mlp_step_f32: null w / X / labels / work");
+  const int64_t P = int64_t(h) * d + h + int64_t(c) * h + c;
+  if (ldw < P || (grad && ldg < P) || (mom && ldm < P) || (alpha && lda < P))
+    return fail(DOL_EINVAL, "dol_mlp_step_f32: ld < P (%lld)", (long long)P);
+  if (ldx_row < d || ldx_agent < int64_t(B - 1) * ldx_row + d || ldy_agent < B)
+    return fail(DOL_EINVAL, "dol_mlp_step_f32: X / labels strides too small");
+  if ((reinterpret_cast<uintptr_t>(w) & 15) || ldw % 4 || (reinterpret_cast<uintptr_t>(X) & 15) || ldx_row % 4 ||
+      ldx_agent % 4)
+    return fail(DOL_EINVAL, "dol_mlp_step_f32: w and X rows must be 16-byte aligned");
+  if (alpha && !theta) return fail(DOL_EINVAL, "dol_mlp_step_f32: alpha without theta");
+  const int mode = (momentum == 0.0f) ? 0 : (first_step ? 1 : 2);
+  if (update && mode != 0 && !mom) return fail(DOL_EINVAL, "dol_mlp_step_f32: momentum needs the mom buffer");
+  if (!update && !grad) return fail(DOL_EINVAL, "dol_mlp_step_f32: update=0 needs a grad buffer to write");
+  MlpArgs a{w, ldw, grad, ldg, mom, ldm, theta, alpha, lda, X, ldx_agent, ldx_row, labels, ldy_agent, loss,
+            B, d, h, c, -lr, momentum, rho, update ? mode : 0, update ? 1 : 0};
+  const size_t lds = static_cast<size_t>(dol_mlp_step_lds_bytes(B, h, c));
+  if (lds > 160 * 1024) return fail(DOL_EINVAL, "dol_mlp_step_f32: %zu B of LDS per agent exceeds 160 KiB", lds);
+  const dim3 grid(static_cast<unsigned>(n_agents)), block(kThreads);
+  const int upd = update ? mode + 1 : 0;
+  float* ws = static_cast<float*>(work);
+  const int64_t n_blk2 = int64_t((d + 31) / 32) * n_agents;
+  if (n_blk2 > (int64_t(1) << 31) - 1) return fail(DOL_EINVAL, "dol_mlp_step_f32: too many W1 tiles for one launch");
+  const dim3 grid2(static_cast<unsigned>(n_blk2));
+  auto go = [&](auto ks, auto upd_c, auto th, auto al) {
+    constexpr int KS = decltype(ks)::value, U = decltype(upd_c)::value;
+    constexpr bool TH = decltype(th)::value, AL = decltype(al)::value;
+    auto fwd = [&](auto kern) {
+      if (lds > 65536)  // above the default dynamic-LDS cap (gfx950 has 160 KiB per CU)
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  static_cast<int>(lds));
+      hipLaunchKernelGGL(kern, grid, block, lds, s, a, ws);
+    };
+    if (h * ((B + 31) / 32) <= 128) fwd(mlp_fwd_kernel<1, U, TH, AL>);
+    else fwd(mlp_fwd_kernel<4, U, TH, AL>);
+    hipLaunchKernelGGL((mlp_dw1_kernel<KS, U, TH, AL>), grid2, block, 0, s, a, ws);
+  };
+  auto by_upd = [&](auto ks, auto th, auto al) {
+    using std::integral_constant;
+    switch (upd) {
+      case 0: go(ks, integral_constant<int, 0>{}, th, al); break;
+      case 1: go(ks, integral_constant<int, 1>{}, th, al); break;
+      case 2: go(ks, integral_constant<int, 2>{}, th, al); break;
+      default: go(ks, integral_constant<int, 3>{}, th, al); break;
+    }
+  };
+  using K16 = std::integral_constant<int, 16>;
+  using K32 = std::integral_constant<int, 32>;
+  using T = std::true_type;
+  using F = std::false_type;
+  if (B <= 32) {
+    if (!theta) by_upd(K16{}, F{}, F{});
+    else if (!alpha) by_upd(K16{}, T{}, F{});
+    else by_upd(K16{}, T{}, T{});
+  } else {
+    if (!theta) by_upd(K32{}, F{}, F{});
+    else if (!alpha) by_upd(K32{}, T{}, F{});
+    else by_upd(K32{}, T{}, T{});
+  }
+  return dol::check_launch("dol_mlp_step_f32");
+}

@@ -10,10 +10,16 @@ whose parameters are rows of an AgentBank (state_dict order: 0.weight [h,d],
   dW1 = dZ1^T X,  db1 = sum_b dZ1
   then one fused SGD / prox / ADMM kernel over every row (dol_prox_admm_sgd_f32)
 
-The GEMMs are strided-batched over the bank rows (batch stride = ld): the
-weights are read in place and dW1/dW2 are written straight into the bank's
-grad rows, no copies.  This is the per-agent loop of DIST/clients.py:34-59
-(one nn.Module forward/backward per agent) batched into one launch per layer.
+`step` runs the whole local iteration of every agent in ONE hand-written
+kernel (dol_mlp_step_f32, csrc/mlp_step.hip): forward and backward GEMMs on
+fp32 MFMA, softmax-CE, and the (prox/ADMM) momentum-SGD update applied to
+each gradient tile in registers, so gradients never round-trip through HBM.
+This is the per-agent loop of DIST/clients.py:34-59 (one nn.Module
+forward/backward/step per agent) batched into one launch.
+
+`forward_backward_torch` keeps the earlier strided-batched formulation
+(torch.bmm over the bank rows) as a second implementation the tests compare
+against; it is not used by `step`.
 """
 from __future__ import annotations
 
@@ -55,8 +61,16 @@ class BatchedMLP:
 
     def forward_backward(self, X: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
         """X [N, B, d] fp32, y [N, B] int64 on the bank's device.  Writes every
-        agent's gradient into the bank's grad rows; returns the per-agent mean
-        cross-entropy [N]."""
+        agent's gradient into the bank's grad rows (fused HIP kernel, no
+        update); returns the per-agent mean cross-entropy [N]."""
+        from . import ops
+        loss = torch.empty(self.bank.n, dtype=torch.float32, device=self.bank.device)
+        ops.mlp_step(self.bank.buffer("x"), X, y, self.d, self.h, self.c, grad=self.bank.buffer("grad"),
+                     loss=loss, update=False)
+        return loss
+
+    def forward_backward_torch(self, X: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+        """Same contract as forward_backward, via torch.bmm (library GEMMs)."""
         n, B = X.shape[0], X.shape[1]
         if n != self.bank.n or X.shape[2] != self.d:
             raise ValueError(f"X must be [{self.bank.n}, B, {self.d}]")
@@ -80,8 +94,23 @@ class BatchedMLP:
         return loss
 
     def step(self, X: torch.Tensor, y: torch.Tensor, lr: float, momentum: float, first_step: bool,
-             theta: Optional[torch.Tensor] = None, rho: float = 0.0, admm: bool = False) -> torch.Tensor:
-        loss = self.forward_backward(X, y)
+             theta: Optional[torch.Tensor] = None, rho: float = 0.0, admm: bool = False,
+             write_grad: bool = False) -> torch.Tensor:
+        """One fused local iteration for every agent (one kernel launch)."""
+        from . import ops
+        b = self.bank
+        loss = torch.empty(b.n, dtype=torch.float32, device=b.device)
+        ops.mlp_step(b.buffer("x"), X, y, self.d, self.h, self.c,
+                     grad=b.buffer("grad") if write_grad else None,
+                     mom=b.buffer("mom", zero=True) if momentum != 0.0 else None,
+                     theta=theta, alpha=b.buffer("alpha", zero=True) if admm else None, loss=loss,
+                     lr=lr, momentum=momentum, rho=rho, first_step=first_step, update=True)
+        return loss
+
+    def step_unfused(self, X: torch.Tensor, y: torch.Tensor, lr: float, momentum: float, first_step: bool,
+                     theta: Optional[torch.Tensor] = None, rho: float = 0.0, admm: bool = False) -> torch.Tensor:
+        """forward_backward_torch + the fused SGD kernel (the pre-fusion path, for comparison)."""
+        loss = self.forward_backward_torch(X, y)
         self.bank.local_step(lr=lr, momentum=momentum, first_step=first_step, theta=theta, rho=rho, admm=admm,
                              write_grad=False)
         return loss

@@ -15,7 +15,7 @@ from ._native import DolNativeError
 
 __all__ = [
     "DolNativeError", "mix_csr", "mix_ring", "mix_dense", "mix_ring_steps", "prox_admm_sgd", "admm_dual", "ordered_mean",
-    "ordered_sum", "stream_copy", "dual_workspace_bytes", "prox_grad", "admm_step_dual",
+    "ordered_sum", "stream_copy", "dual_workspace_bytes", "prox_grad", "admm_step_dual", "mlp_step",
 ]
 
 
@@ -285,3 +285,70 @@ def stream_copy(src: torch.Tensor, dst: torch.Tensor) -> torch.Tensor:
         raise ValueError("stream_copy: contiguous tensors of equal size required")
     _native.call("dol_stream_copy_f32", src.data_ptr(), dst.data_ptr(), src.numel(), _stream(src))
     return dst
+
+
+def mlp_step(w: torch.Tensor, X: torch.Tensor, y: torch.Tensor, d: int, h: int, c: int,
+             grad: Optional[torch.Tensor] = None, mom: Optional[torch.Tensor] = None,
+             theta: Optional[torch.Tensor] = None, alpha: Optional[torch.Tensor] = None,
+             loss: Optional[torch.Tensor] = None, lr: float = 0.01, momentum: float = 0.0, rho: float = 0.0,
+             first_step: bool = False, update: bool = True,
+             work: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+    """Fused forward + CE + backward + (prox/ADMM) momentum-SGD step of every
+    agent's MLP Linear(d,h)-ReLU-Linear(h,c) (rows of w, state_dict order).
+
+    X [n, B, d] fp32, y [n, B] int64.  update=False only writes the raw
+    gradients into grad.  Reference: DIST/clients.py:34-59 (one local
+    iteration per agent), DEC/clients.py:101-139 (prox / ADMM terms)."""
+    P = h * d + h + c * h + c
+    n = w.shape[0]
+    ldw = _check_rows("w", w, P)
+    if X.device != w.device or X.dtype != torch.float32 or X.dim() != 3 or X.shape[0] != n or X.shape[2] != d:
+        raise ValueError(f"X: expected float32 [{n}, B, {d}] on {w.device}")
+    if X.stride(2) != 1:
+        raise ValueError("X: samples must be contiguous")
+    B = X.shape[1]
+    if y.device != w.device or y.dtype != torch.int64 or tuple(y.shape) != (n, B) or (B > 1 and y.stride(1) != 1):
+        raise ValueError(f"y: expected int64 [{n}, {B}] on {w.device}")
+    ldg = _check_rows("grad", grad, P) if grad is not None else 0
+    ldm = 0
+    if update and momentum != 0.0:
+        if mom is None:
+            raise ValueError("momentum != 0 needs mom")
+        ldm = _check_rows("mom", mom, P)
+    lda = 0
+    if alpha is not None:
+        if theta is None:
+            raise ValueError("alpha needs theta")
+        lda = _check_rows("alpha", alpha, P)
+    _check_vec("theta", theta, P, w.device)
+    for nm, t in (("grad", grad), ("mom", mom if ldm else None), ("alpha", alpha)):
+        if t is not None and t.shape[0] < n:
+            raise ValueError(f"{nm} has fewer rows than w")
+    if loss is not None and (loss.device != w.device or loss.dtype != torch.float32 or loss.numel() < n
+                             or not loss.is_contiguous()):
+        raise ValueError(f"loss: expected a contiguous float32 [{n}] on {w.device}")
+    wbytes = int(_native.lib().dol_mlp_step_workspace_bytes(n, B, h))
+    if work is None:
+        work = _workspace(w.device, wbytes)
+    elif work.device != w.device or work.numel() * work.element_size() < wbytes:
+        raise ValueError(f"work: need {wbytes} bytes on {w.device}")
+    ldxa = X.stride(0) if n > 1 else B * X.stride(1)
+    ldxb = X.stride(1) if B > 1 else d
+    _native.call("dol_mlp_step_f32", w.data_ptr(), ldw, _ptr(grad), ldg, _ptr(mom) if ldm else None, ldm,
+                 _ptr(theta), _ptr(alpha), lda, X.data_ptr(), ldxa, ldxb, y.data_ptr(),
+                 y.stride(0) if n > 1 else B, _ptr(loss), n, B, d, h, c, float(lr), float(momentum), float(rho),
+                 int(bool(first_step)), int(bool(update)), work.data_ptr(), _stream(w))
+    return loss
+
+
+_WORK = {}
+
+
+def _workspace(device, nbytes: int) -> torch.Tensor:
+    """Per-device scratch, grown on demand and reused (stream-ordered on the
+    current stream like every other op)."""
+    t = _WORK.get(device)
+    if t is None or t.numel() < nbytes:
+        t = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device)
+        _WORK[device] = t
+    return t

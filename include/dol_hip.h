@@ -184,6 +184,37 @@ int dol_ordered_sum_f32(const float* W, int64_t ldw, const int32_t* order,
                         int32_t m, int64_t P, const float* acc_in,
                         float* acc_out, float scale, hipStream_t s);
 
+/*
+ * One fused local step of n_agents per-agent MLPs  Linear(d,h) -> ReLU -> Linear(h,c)
+ * with CrossEntropyLoss (mean over the batch), parameters = rows of w in
+ * state_dict order [W1 (h x d), b1 (h), W2 (c x h), b2 (c)], P = h*d + h + c*h + c.
+ * Replaces, for every agent at once, one iteration of the reference's local loop
+ *   DIST/clients.py:34-59   forward, loss, backward, optimizer.step()
+ *   DEC/clients.py:101-139  (FedProx / FedADMM gradient terms, theta / alpha)
+ * i.e. forward + backward on fp32 MFMA (v_mfma_f32_32x32x2_f32) and the update of
+ * dol_prox_admm_sgd_f32 (same rounding) applied to each gradient tile in registers.
+ * X: agent k's batch at X + k*ldx_agent, sample b at + b*ldx_row (d floats, 16-B
+ * aligned); labels: int64 [k*ldy_agent + b] in [0, c) (out of range -> NaN loss).
+ * update == 0: only write the raw gradients to grad (forward_backward); otherwise
+ * update w (and mom), and store g' into grad when grad != NULL.  loss: [n_agents]
+ * per-agent mean CE, or NULL.  work: device scratch of
+ * dol_mlp_step_workspace_bytes(n_agents, B, h) bytes (holds dZ1 between the two
+ * launches the step enqueues).  Limits: 1 <= B <= 64, h % 32 == 0 and h <= 256,
+ * c <= 32, d % 4 == 0.  GEMM numerics are fp32 fma chains (tolerance, not
+ * bit-exact vs torch CPU).
+ */
+int dol_mlp_step_f32(float* w, int64_t ldw, float* grad, int64_t ldg, float* mom, int64_t ldm,
+                     const float* theta, const float* alpha, int64_t lda,
+                     const float* X, int64_t ldx_agent, int64_t ldx_row,
+                     const int64_t* labels, int64_t ldy_agent, float* loss,
+                     int32_t n_agents, int32_t B, int32_t d, int32_t h, int32_t c,
+                     float lr, float momentum, float rho, int first_step, int update,
+                     void* work, hipStream_t s);
+/* Scratch bytes dol_mlp_step_f32 needs (n_agents * B * h floats). */
+int64_t dol_mlp_step_workspace_bytes(int32_t n_agents, int32_t B, int32_t h);
+/* Dynamic LDS bytes the MLP step uses per workgroup (one agent). */
+int64_t dol_mlp_step_lds_bytes(int32_t B, int32_t h, int32_t c);
+
 /* Streaming copy dst = src (n floats): HBM calibration kernel for roofline. */
 int dol_stream_copy_f32(const float* src, float* dst, int64_t n, hipStream_t s);
 

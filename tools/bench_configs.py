@@ -50,16 +50,13 @@ def mlp_round(N, d, h, c, B, p_edge, reps, dev):
     X = torch.randn(N, B, d, device=dev)
     y = torch.randint(0, c, (N, B), device=dev)
     ev = {k: [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
-          for k in ("fwd_bwd", "sgd", "mix")}
+          for k in ("local", "mix")}
 
     def one(k=None):
         r = (lambda nm, i: ev[nm][k][i].record()) if k is not None else (lambda nm, i: None)
-        r("fwd_bwd", 0)
-        mlp.forward_backward(X, y)
-        r("fwd_bwd", 1)
-        r("sgd", 0)
-        bank.local_step(lr=0.05, momentum=0.5, first_step=False, write_grad=False)
-        r("sgd", 1)
+        r("local", 0)
+        mlp.step(X, y, lr=0.05, momentum=0.5, first_step=False)   # fused fwd+CE+bwd+SGD (one kernel)
+        r("local", 1)
         r("mix", 0)
         bank.mix(plan)
         r("mix", 1)
@@ -72,13 +69,31 @@ def mlp_round(N, d, h, c, B, p_edge, reps, dev):
     torch.cuda.synchronize()
     el = (time.perf_counter() - t0) / reps
     ms = {k: sum(a.elapsed_time(b) for a, b in v) / reps for k, v in ev.items()}
+
+    # the pre-fusion path (torch.bmm fwd/bwd + the fused SGD kernel), same data, for comparison
+    def unfused():
+        mlp.step_unfused(X, y, lr=0.05, momentum=0.5, first_step=False)
+    for _ in range(2):
+        unfused()
+    torch.cuda.synchronize()
+    s_, e_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s_.record()
+    for _ in range(reps):
+        unfused()
+    e_.record()
+    torch.cuda.synchronize()
+    ms["local_unfused"] = s_.elapsed_time(e_) / reps
+
     P = bank.P
     flops_fb = 2.0 * N * B * (d * h + h * c) * 3  # fwd + two backward GEMMs per layer
+    local_bytes = N * (4 * P + B * d) * 4           # w, mom in + out, X in (compulsory)
     out = {"workload": "config5: ER p=%.2f dense MFMA mix + batched MLP %d-%d-%d local step" % (p_edge, d, h, c),
            "agents": N, "params": P, "batch": B, "ms_per_round": el * 1e3, "rounds_per_s": 1 / el, "kernel_ms": ms,
            "mix_TFLOPs": 2.0 * N * N * P / (ms["mix"] / 1e3) / 1e12,
-           "fwd_bwd_TFLOPs": flops_fb / (ms["fwd_bwd"] / 1e3) / 1e12,
-           "sgd_GBps": 5 * N * P * 4 / (ms["sgd"] / 1e3) / 1e9}
+           "local_TFLOPs": flops_fb / (ms["local"] / 1e3) / 1e12,
+           "local_GBps": local_bytes / (ms["local"] / 1e3) / 1e9,
+           "local_frac_of_8TBps": local_bytes / (ms["local"] / 1e3) / 1e9 / 8000.0,
+           "local_speedup_vs_unfused": ms["local_unfused"] / ms["local"]}
     print(json.dumps(out), flush=True)
     del bank, mlp, plan, X, y
     torch.cuda.empty_cache()
