@@ -104,6 +104,71 @@ __device__ __forceinline__ f4 vdiv(f4 a, float s) {
   return f4{a.x / s, a.y / s, a.z / s, a.w / s};
 }
 
+// ----------------------------------------------------------------------------
+// Mixing epilogues.  NoEpi: Y = W X (the gossip round).  DgdEpi: then `steps`
+// local momentum-SGD iterations per agent on a separable synthetic loss —
+// BASELINE config 3, decentralised gradient descent in the reference's round
+// order (DIST/simulators.py:147-162: consensus, then local_update with the
+// optimizer of DIST/clients.py:43-49) — so a round streams X, the targets and
+// the momentum once.  Rounding as oracle_dgd_local_f32:
+//   OBJ 0 least squares  g = x - t;   OBJ 1 logistic  g = -t / (1 + exp(t x))
+//   MODE 0 plain SGD; 1 momentum, first step (buf = g); 2 momentum (buf = buf*mom + g)
+//   x = fma(-lr, d, x)
+// load() is issued with the mixing loads; apply() runs after the mix.
+// ----------------------------------------------------------------------------
+struct Empty {};
+struct NoEpi {
+  template <typename V> __device__ __forceinline__ Empty load(int, int64_t) const { return {}; }
+  template <typename V> __device__ __forceinline__ V apply(V y, Empty, int, int64_t) const { return y; }
+};
+
+template <typename V> struct DgdState { V t, b; };
+
+template <int OBJ, int MODE>
+struct DgdEpi {
+  const float* __restrict__ T; int64_t ldt;
+  float* __restrict__ M; int64_t ldm;
+  float neg_lr, mom;
+  int steps;
+
+  template <typename V> __device__ __forceinline__ DgdState<V> load(int r, int64_t cf) const {
+    DgdState<V> st;
+    st.t = *reinterpret_cast<const V*>(T + int64_t(r) * ldt + cf);
+    if constexpr (MODE == 2) st.b = *reinterpret_cast<const V*>(M + int64_t(r) * ldm + cf);
+    else st.b = vzero(V{});
+    return st;
+  }
+  __device__ __forceinline__ float local(float x, float t, float& b) const {
+    for (int s = 0; s < steps; ++s) {
+      float g;
+      if constexpr (OBJ == 0) g = x - t;
+      else g = -t / (1.0f + expf(t * x));
+      float d = g;
+      if constexpr (MODE != 0) {
+        if (MODE == 1 && s == 0) b = g;
+        else b = b * mom + g;
+        d = b;
+      }
+      x = __builtin_fmaf(neg_lr, d, x);
+    }
+    return x;
+  }
+  template <typename V> __device__ __forceinline__ V apply(V y, DgdState<V> st, int r, int64_t cf) const {
+    if constexpr (Vec<V>::W == 1) {
+      y = local(y, st.t, st.b);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float bj = st.b[j];
+        y[j] = local(y[j], st.t[j], bj);
+        st.b[j] = bj;
+      }
+    }
+    if constexpr (MODE != 0) __builtin_nontemporal_store(st.b, reinterpret_cast<V*>(M + int64_t(r) * ldm + cf));
+    return y;
+  }
+};
+
 template <typename V, bool NT>
 __device__ __forceinline__ V ldv(const V* p) {
   if constexpr (NT) return __builtin_nontemporal_load(p);
@@ -126,12 +191,12 @@ __device__ __forceinline__ void stv(V* p, V v) {
 // tile) are re-read from L2: vertically adjacent tiles are n_col_tiles
 // blocks apart (a multiple of 8 -> same XCD) and co-resident.
 // ----------------------------------------------------------------------------
-template <typename V, int PF, bool NT_LOAD, bool NT_STORE>
+template <typename V, int PF, bool NT_LOAD, bool NT_STORE, class Epi = NoEpi>
 __global__ __launch_bounds__(kThreads) void ring_mix_kernel(
     const float* __restrict__ X, int64_t ldx, float* __restrict__ Y, int64_t ldy,
     int n_rows, int64_t c_off, int64_t ncols_v, int64_t n_col_tiles, int rows_per_block,
     const float* __restrict__ halo_prev, const float* __restrict__ halo_next,
-    const float* __restrict__ wprev, const float* __restrict__ wnext) {
+    const float* __restrict__ wprev, const float* __restrict__ wnext, Epi epi) {
   // 32-bit block decomposition (grids are < 2^24 blocks); column tile fastest,
   // so co-resident workgroups share rows and the halo re-reads hit L2
   const uint32_t b = blockIdx.x;
@@ -163,6 +228,8 @@ __global__ __launch_bounds__(kThreads) void ring_mix_kernel(
       const int r = i + k;
       if (r < r1) {
         V out = axpy0(wprev[r], q[k], wnext[r], q[k + 2]);
+        const int64_t cf = c_off + c * Vec<V>::W;
+        out = epi.apply(out, epi.template load<V>(r, cf), r, cf);
         stv<V, NT_STORE>(reinterpret_cast<V*>(Y + int64_t(r) * ldy + c_off) + c, out);
       }
     }
@@ -186,11 +253,12 @@ __global__ __launch_bounds__(kThreads) void ring_mix_kernel(
 #define DOL_GPTR(p) ((const __attribute__((address_space(1))) void*)(p))
 #define DOL_LPTR(p) ((__attribute__((address_space(3))) void*)(p))
 
-template <int R>
+template <int R, class Epi = NoEpi>
 __global__ __launch_bounds__(kThreads) void ring_mix_dma_kernel(
     const float* __restrict__ X, int64_t ldx, float* __restrict__ Y, int64_t ldy, int n_rows,
     int64_t ncols_v, int64_t n_col_tiles, const float* __restrict__ halo_prev,
-    const float* __restrict__ halo_next, const float* __restrict__ wprev, const float* __restrict__ wnext) {
+    const float* __restrict__ halo_next, const float* __restrict__ wprev, const float* __restrict__ wnext,
+    Epi epi) {
   __shared__ __attribute__((aligned(16))) float lds[kThreads / 64][R + 2][256];
   const uint32_t b = blockIdx.x;
   const uint32_t nct = static_cast<uint32_t>(n_col_tiles);
@@ -208,6 +276,9 @@ __global__ __launch_bounds__(kThreads) void ring_mix_dma_kernel(
     const int r = min(r0 - 1 + k, r1);
     __builtin_amdgcn_global_load_lds(DOL_GPTR(row(r) + 4 * c), DOL_LPTR(&lds[wave][k][0]), 16, 0, 0);
   }
+  decltype(epi.template load<f4>(0, 0)) es[R];  // epilogue operands ride with the DMA
+#pragma unroll
+  for (int k = 0; k < R; ++k) es[k] = epi.template load<f4>(min(r0 + k, r1 - 1), 4 * c);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   f4 v[R + 2];
 #pragma unroll
@@ -216,7 +287,8 @@ __global__ __launch_bounds__(kThreads) void ring_mix_dma_kernel(
   for (int k = 0; k < R; ++k) {
     const int r = r0 + k;
     if (r < r1)
-      __builtin_nontemporal_store(axpy0(wprev[r], v[k], wnext[r], v[k + 2]), reinterpret_cast<f4*>(Y + int64_t(r) * ldy) + c);
+      __builtin_nontemporal_store(epi.apply(axpy0(wprev[r], v[k], wnext[r], v[k + 2]), es[k], r, 4 * c),
+                                  reinterpret_cast<f4*>(Y + int64_t(r) * ldy) + c);
   }
 }
 
@@ -267,11 +339,11 @@ __global__ __launch_bounds__(kThreads) void ring_steps_kernel(
 // one column tile are in flight together: a neighbour row segment fetched
 // from HBM by one workgroup is re-read from L2 / Infinity Cache by the others.
 // ----------------------------------------------------------------------------
-template <typename V, int RPB>
+template <typename V, int RPB, class Epi = NoEpi>
 __global__ __launch_bounds__(kThreads) void csr_mix_kernel(
     const float* __restrict__ X, int64_t ldx, float* __restrict__ Y, int64_t ldy, int n_rows,
     int64_t c_off, int64_t ncols_v, int64_t n_row_groups, const int32_t* __restrict__ rowptr,
-    const int32_t* __restrict__ col, const float* __restrict__ val) {
+    const int32_t* __restrict__ col, const float* __restrict__ val, Epi epi) {
   const int64_t b = blockIdx.x;
   const int rg = static_cast<int>(b % n_row_groups);
   const int64_t ct = b / n_row_groups;
@@ -280,7 +352,9 @@ __global__ __launch_bounds__(kThreads) void csr_mix_kernel(
   const int r0 = rg * RPB;
   const int r1 = min(r0 + RPB, n_rows);
   const V* xb = reinterpret_cast<const V*>(X + c_off) + c;
+  const int64_t cf = c_off + c * Vec<V>::W;
   for (int r = r0; r < r1; ++r) {
+    const auto es = epi.template load<V>(r, cf);
     const int e0 = rowptr[r];
     const int e1 = rowptr[r + 1];
     V acc = vzero(V{});
@@ -296,6 +370,7 @@ __global__ __launch_bounds__(kThreads) void csr_mix_kernel(
       acc = fmac(acc, val[e + 3], x3);
     }
     for (; e < e1; ++e) acc = fmac(acc, val[e], xb[int64_t(col[e]) * (ldx / Vec<V>::W)]);
+    acc = epi.apply(acc, es, r, cf);
     __builtin_nontemporal_store(acc, reinterpret_cast<V*>(Y + int64_t(r) * ldy + c_off) + c);
   }
 }
@@ -310,11 +385,11 @@ __global__ __launch_bounds__(kThreads) void csr_mix_kernel(
 // other block->XCD mapping gives the same results.  Measured at 8192 x 2^20,
 // d = 4 (tools/membench6.hip): 4.04 TB/s vs 3.0 with 4 KiB tiles whose 32 MiB
 // slabs re-read through the Infinity Cache.
-template <int W, int PASSES>
+template <int W, int PASSES, class Epi = NoEpi>
 __global__ __launch_bounds__(kThreads) void csr_xcd_kernel(
     const float* __restrict__ X, int64_t ldx, float* __restrict__ Y, int64_t ldy, int n_rows,
     uint32_t nrb, uint32_t ntiles, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
-    const float* __restrict__ val) {
+    const float* __restrict__ val, Epi epi) {
   constexpr int ROWS = kThreads / W;
   constexpr int RB = ROWS * PASSES;
   const uint32_t b = blockIdx.x;
@@ -330,6 +405,7 @@ __global__ __launch_bounds__(kThreads) void csr_xcd_kernel(
   for (int p = 0; p < PASSES; ++p) {
     const int r = int(rb) * RB + p * ROWS + lane_r;
     if (r < n_rows) {
+      const auto es = epi.template load<f4>(r, 4 * c);
       f4 acc = f4{0.f, 0.f, 0.f, 0.f};
       const int e1 = rowptr[r + 1];
       int e = rowptr[r];
@@ -342,6 +418,7 @@ __global__ __launch_bounds__(kThreads) void csr_xcd_kernel(
         acc = fmac(acc, val[e + 3], x3);
       }
       for (; e < e1; ++e) acc = fmac(acc, val[e], xb[int64_t(col[e]) * ldv]);
+      acc = epi.apply(acc, es, r, 4 * c);
       __builtin_nontemporal_store(acc, reinterpret_cast<f4*>(Y + int64_t(r) * ldy) + c);
     }
   }
@@ -691,15 +768,15 @@ inline ColSplit split_cols(int64_t P, bool vec_ok) {
 
 inline bool row_vec_ok(const void* base, int64_t ld) { return base == nullptr || (aligned16(base) && (ld % 4) == 0); }
 
-template <typename V, int PF, bool NTL, bool NTS>
+template <typename V, int PF, bool NTL, bool NTS, class Epi = NoEpi>
 void launch_ring(const float* X, int64_t ldx, float* Y, int64_t ldy, int n_rows, int64_t c_off,
                  int64_t ncols_v, int rpb, const float* hp, const float* hn, const float* wp,
-                 const float* wn, hipStream_t s) {
+                 const float* wn, hipStream_t s, const Epi& epi = Epi{}) {
   const int64_t n_col_tiles = cdiv(ncols_v, kThreads);
   const int64_t n_rg = cdiv(n_rows, rpb);
   const int64_t grid = n_col_tiles * n_rg;
-  hipLaunchKernelGGL((ring_mix_kernel<V, PF, NTL, NTS>), dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, s, X,
-                     ldx, Y, ldy, n_rows, c_off, ncols_v, n_col_tiles, rpb, hp, hn, wp, wn);
+  hipLaunchKernelGGL((ring_mix_kernel<V, PF, NTL, NTS, Epi>), dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, s,
+                     X, ldx, Y, ldy, n_rows, c_off, ncols_v, n_col_tiles, rpb, hp, hn, wp, wn, epi);
 }
 
 template <typename V>
@@ -730,14 +807,14 @@ int ring_rows_per_block(int n_rows, int64_t n_col_tiles, int pf) {
   return pf < 4 ? pf : 4;  // see the ring kernel comment: 4 rows per tile, all loads up front
 }
 
-template <typename V, int RPB>
+template <typename V, int RPB, class Epi = NoEpi>
 void launch_csr(const float* X, int64_t ldx, float* Y, int64_t ldy, int n_rows, int64_t c_off,
                 int64_t ncols_v, const int32_t* rowptr, const int32_t* col, const float* val,
-                hipStream_t s) {
+                hipStream_t s, const Epi& epi = Epi{}) {
   const int64_t n_col_tiles = cdiv(ncols_v, kThreads);
   const int64_t n_rg = cdiv(n_rows, RPB);
-  hipLaunchKernelGGL((csr_mix_kernel<V, RPB>), dim3(static_cast<unsigned>(n_col_tiles * n_rg)), dim3(kThreads), 0, s,
-                     X, ldx, Y, ldy, n_rows, c_off, ncols_v, n_rg, rowptr, col, val);
+  hipLaunchKernelGGL((csr_mix_kernel<V, RPB, Epi>), dim3(static_cast<unsigned>(n_col_tiles * n_rg)), dim3(kThreads), 0,
+                     s, X, ldx, Y, ldy, n_rows, c_off, ncols_v, n_rg, rowptr, col, val, epi);
 }
 
 template <typename V, bool TH, bool AL, int MODE, bool WG>
@@ -778,6 +855,90 @@ void dispatch_prox(bool th, bool al, int mode, bool wg, float* w, int64_t ldw, f
   else dispatch_prox_mode<V, true, true>(mode, wg, w, ldw, b, ldb, g, ldg, tp, ap, lda, rho, lr, mom, n, c_off, nc, s);
 }
 
+
+// Shared bodies of the plain and epilogue (DGD) forms of the two sparse mixes.
+template <class Epi>
+int mix_csr_impl(const char* nm, const float* X, int64_t ldx, int32_t x_rows, float* Y, int64_t ldy,
+                 int32_t n_rows, int64_t P, const int32_t* rowptr, const int32_t* col, const float* val,
+                 const Epi& epi, bool epi_vec_ok, hipStream_t s) {
+  if (n_rows < 0 || P < 0 || x_rows < 0) return fail(DOL_EINVAL, "%s: negative size", nm);
+  if (n_rows == 0 || P == 0) { g_err[0] = '\0'; return DOL_OK; }
+  if (!X || !Y || !rowptr || (!col && x_rows > 0) || (!val && x_rows > 0))
+    return fail(DOL_EINVAL, "%s: null pointer", nm);
+  if (ldx < P || ldy < P) return fail(DOL_EINVAL, "%s: ld < P", nm);
+  if (X == Y) return fail(DOL_EINVAL, "%s: X and Y alias (Jacobi mix needs two buffers)", nm);
+  const bool vec_ok = row_vec_ok(X, ldx) && row_vec_ok(Y, ldy) && epi_vec_ok;
+  const ColSplit cs = split_cols(P, vec_ok);
+  constexpr int RPB = 16;
+  constexpr int XW = 32, XPASSES = 2;  // XCD-pinned tiles: 512 B of a row, 16 rows per block
+  const int mode = env_int("DOL_CSR_MODE", -1);  // 0 = 4 KiB tiles, 1 = XCD-pinned
+  const bool use_xcd = cs.n4 >= XW && (mode == 1 || (mode < 0 && n_rows >= 512));
+  if (cdiv(cs.n4, kThreads) * cdiv(n_rows, RPB) > kMaxBlocks)
+    return fail(DOL_EINVAL, "%s: problem too large for one launch", nm);
+  int64_t done4 = 0;
+  if (use_xcd) {
+    const int64_t ntiles = cs.n4 / XW;
+    const int64_t nrb = cdiv(n_rows, (kThreads / XW) * XPASSES);
+    const int64_t grid = cdiv(ntiles, 8) * 8 * nrb;
+    if (grid > kMaxBlocks * 8) return fail(DOL_EINVAL, "%s: problem too large for one launch", nm);
+    hipLaunchKernelGGL((csr_xcd_kernel<XW, XPASSES, Epi>), dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, s, X,
+                       ldx, Y, ldy, n_rows, static_cast<uint32_t>(nrb), static_cast<uint32_t>(ntiles), rowptr, col, val,
+                       epi);
+    done4 = ntiles * XW;
+  }
+  if (cs.n4 > done4)  // column offset through c_off so the epilogue sees absolute columns
+    launch_csr<f4, RPB, Epi>(X, ldx, Y, ldy, n_rows, done4 * 4, cs.n4 - done4, rowptr, col, val, s, epi);
+  if (cs.tail > 0)
+    launch_csr<float, RPB, Epi>(X, ldx, Y, ldy, n_rows, cs.n4 * 4, cs.tail, rowptr, col, val, s, epi);
+  return check_launch(nm);
+}
+
+template <class Epi>
+int mix_ring_impl(const char* nm, const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t n_rows, int64_t P,
+                  const float* halo_prev, const float* halo_next, const float* w_prev, const float* w_next,
+                  const Epi& epi, bool epi_vec_ok, hipStream_t s) {
+  constexpr bool kPlain = std::is_same<Epi, NoEpi>::value;
+  if (n_rows < 0 || P < 0) return fail(DOL_EINVAL, "%s: negative size", nm);
+  if (n_rows == 0 || P == 0) { g_err[0] = '\0'; return DOL_OK; }
+  if (!X || !Y || !w_prev || !w_next) return fail(DOL_EINVAL, "%s: null pointer", nm);
+  if (ldx < P || ldy < P) return fail(DOL_EINVAL, "%s: ld < P", nm);
+  if (X == Y) return fail(DOL_EINVAL, "%s: X and Y alias (Jacobi mix needs two buffers)", nm);
+  if ((halo_prev == nullptr) != (halo_next == nullptr)) return fail(DOL_EINVAL, "%s: pass both halos or neither", nm);
+  if (!halo_prev) {
+    if (n_rows < 3) return fail(DOL_EINVAL, "%s: wrap-around ring needs n_rows >= 3", nm);
+    halo_prev = X + int64_t(n_rows - 1) * ldx;
+    halo_next = X;
+  }
+  const bool vec_ok = row_vec_ok(X, ldx) && row_vec_ok(Y, ldy) && aligned16(halo_prev) && aligned16(halo_next) &&
+                      epi_vec_ok;
+  const ColSplit cs = split_cols(P, vec_ok);
+  if (cs.n4 > 0) {
+    const int64_t nct = cdiv(cs.n4, kThreads);
+    bool dma = true;
+    if constexpr (kPlain) dma = env_int("DOL_RING_DMA", 1) != 0;
+    if (dma) {
+      constexpr int R = 4;
+      if (nct * cdiv(n_rows, R) > kMaxBlocks) return fail(DOL_EINVAL, "%s: problem too large for one launch", nm);
+      hipLaunchKernelGGL((ring_mix_dma_kernel<R, Epi>), dim3(static_cast<unsigned>(nct * cdiv(n_rows, R))), dim3(kThreads),
+                         0, s, X, ldx, Y, ldy, n_rows, cs.n4, nct, halo_prev, halo_next, w_prev, w_next, epi);
+    } else if constexpr (kPlain) {
+      const int pf = env_int("DOL_RING_PF", 4);
+      const int nt = env_int("DOL_RING_NT", 2);
+      const int rpb = ring_rows_per_block(n_rows, nct, pf);
+      if (nct * cdiv(n_rows, rpb) > kMaxBlocks) return fail(DOL_EINVAL, "%s: problem too large for one launch", nm);
+      launch_ring_variant<f4>(pf, nt, X, ldx, Y, ldy, n_rows, 0, cs.n4, rpb, halo_prev, halo_next, w_prev, w_next, s);
+    }
+  }
+  if (cs.tail > 0) {
+    const int rpb = ring_rows_per_block(n_rows, cdiv(cs.tail, kThreads), 4);
+    if (cdiv(cs.tail, kThreads) * cdiv(n_rows, rpb) > kMaxBlocks)
+      return fail(DOL_EINVAL, "%s: problem too large for one launch", nm);
+    launch_ring<float, 4, false, true, Epi>(X, ldx, Y, ldy, n_rows, cs.n4 * 4, cs.tail, rpb, halo_prev, halo_next,
+                                            w_prev, w_next, s, epi);
+  }
+  return check_launch(nm);
+}
+
 }  // namespace
 
 // ============================================================================
@@ -792,78 +953,87 @@ const char* dol_last_error(void) { return g_err; }
 int dol_mix_csr_f32(const float* X, int64_t ldx, int32_t x_rows, float* Y, int64_t ldy,
                     int32_t n_rows, int64_t P, const int32_t* rowptr, const int32_t* col,
                     const float* val, hipStream_t s) {
-  if (n_rows < 0 || P < 0 || x_rows < 0) return fail(DOL_EINVAL, "dol_mix_csr_f32: negative size");
-  if (n_rows == 0 || P == 0) { g_err[0] = '\0'; return DOL_OK; }
-  if (!X || !Y || !rowptr || (!col && x_rows > 0) || (!val && x_rows > 0))
-    return fail(DOL_EINVAL, "dol_mix_csr_f32: null pointer");
-  if (ldx < P || ldy < P) return fail(DOL_EINVAL, "dol_mix_csr_f32: ld < P");
-  if (X == Y) return fail(DOL_EINVAL, "dol_mix_csr_f32: X and Y alias (Jacobi mix needs two buffers)");
-  const bool vec_ok = row_vec_ok(X, ldx) && row_vec_ok(Y, ldy);
-  const ColSplit cs = split_cols(P, vec_ok);
-  constexpr int RPB = 16;
-  constexpr int XW = 32, XPASSES = 2;  // XCD-pinned tiles: 512 B of a row, 16 rows per block
-  const int mode = env_int("DOL_CSR_MODE", -1);  // 0 = 4 KiB tiles, 1 = XCD-pinned
-  const bool use_xcd = cs.n4 >= XW && (mode == 1 || (mode < 0 && n_rows >= 512));
-  if (cdiv(cs.n4, kThreads) * cdiv(n_rows, RPB) > kMaxBlocks)
-    return fail(DOL_EINVAL, "dol_mix_csr_f32: problem too large for one launch");
-  int64_t done4 = 0;
-  if (use_xcd) {
-    const int64_t ntiles = cs.n4 / XW;
-    const int64_t nrb = cdiv(n_rows, (kThreads / XW) * XPASSES);
-    const int64_t grid = cdiv(ntiles, 8) * 8 * nrb;
-    if (grid > kMaxBlocks * 8) return fail(DOL_EINVAL, "dol_mix_csr_f32: problem too large for one launch");
-    hipLaunchKernelGGL((csr_xcd_kernel<XW, XPASSES>), dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, s, X, ldx, Y,
-                       ldy, n_rows, static_cast<uint32_t>(nrb), static_cast<uint32_t>(ntiles), rowptr, col, val);
-    done4 = ntiles * XW;
-  }
-  if (cs.n4 > done4)
-    launch_csr<f4, RPB>(X + done4 * 4, ldx, Y + done4 * 4, ldy, n_rows, 0, cs.n4 - done4, rowptr, col, val, s);
-  if (cs.tail > 0)
-    launch_csr<float, RPB>(X, ldx, Y, ldy, n_rows, cs.n4 * 4, cs.tail, rowptr, col, val, s);
-  return check_launch("dol_mix_csr_f32");
+  return mix_csr_impl("dol_mix_csr_f32", X, ldx, x_rows, Y, ldy, n_rows, P, rowptr, col, val, NoEpi{}, true, s);
 }
 
 int dol_mix_ring_f32(const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t n_rows, int64_t P,
                      const float* halo_prev, const float* halo_next, const float* w_prev,
                      const float* w_next, hipStream_t s) {
-  if (n_rows < 0 || P < 0) return fail(DOL_EINVAL, "dol_mix_ring_f32: negative size");
-  if (n_rows == 0 || P == 0) { g_err[0] = '\0'; return DOL_OK; }
-  if (!X || !Y || !w_prev || !w_next) return fail(DOL_EINVAL, "dol_mix_ring_f32: null pointer");
-  if (ldx < P || ldy < P) return fail(DOL_EINVAL, "dol_mix_ring_f32: ld < P");
-  if (X == Y) return fail(DOL_EINVAL, "dol_mix_ring_f32: X and Y alias (Jacobi mix needs two buffers)");
-  if ((halo_prev == nullptr) != (halo_next == nullptr))
-    return fail(DOL_EINVAL, "dol_mix_ring_f32: pass both halos or neither");
-  if (!halo_prev) {
-    if (n_rows < 3) return fail(DOL_EINVAL, "dol_mix_ring_f32: wrap-around ring needs n_rows >= 3");
-    halo_prev = X + int64_t(n_rows - 1) * ldx;
-    halo_next = X;
+  return mix_ring_impl("dol_mix_ring_f32", X, ldx, Y, ldy, n_rows, P, halo_prev, halo_next, w_prev, w_next,
+                       NoEpi{}, true, s);
+}
+
+}  // extern "C"
+
+namespace {
+// validation + dispatch of the BASELINE config-3 round (mix + local steps)
+struct DgdArgs {
+  const float* T; int64_t ldt; float* M; int64_t ldm;
+  int32_t objective, steps; float lr, momentum; int first_step;
+};
+
+int check_dgd(const char* nm, const DgdArgs& d, int64_t P, bool* evec, int* mode) {
+  if (!d.T) return fail(DOL_EINVAL, "%s: null target", nm);
+  if (d.objective != 0 && d.objective != 1) return fail(DOL_EINVAL, "%s: objective must be 0 (least squares) or 1 (logistic)", nm);
+  if (d.steps < 1) return fail(DOL_EINVAL, "%s: local_steps must be >= 1", nm);
+  if (d.ldt < P) return fail(DOL_EINVAL, "%s: ldt < P", nm);
+  *mode = (d.momentum == 0.0f) ? 0 : (d.first_step ? 1 : 2);
+  if (*mode != 0 && (!d.M || d.ldm < P)) return fail(DOL_EINVAL, "%s: momentum needs a momentum buffer with ldm >= P", nm);
+  *evec = row_vec_ok(d.T, d.ldt) && (*mode == 0 || row_vec_ok(d.M, d.ldm));
+  return DOL_OK;
+}
+
+template <class F>
+int with_dgd_epi(const DgdArgs& d, int mode, F&& f) {
+  auto mk = [&](auto obj, auto md) {
+    return f(DgdEpi<decltype(obj)::value, decltype(md)::value>{d.T, d.ldt, d.M, d.ldm, -d.lr, d.momentum, d.steps});
+  };
+  using std::integral_constant;
+  if (d.objective == 0) {
+    if (mode == 0) return mk(integral_constant<int, 0>{}, integral_constant<int, 0>{});
+    if (mode == 1) return mk(integral_constant<int, 0>{}, integral_constant<int, 1>{});
+    return mk(integral_constant<int, 0>{}, integral_constant<int, 2>{});
   }
-  const bool vec_ok = row_vec_ok(X, ldx) && row_vec_ok(Y, ldy) && aligned16(halo_prev) && aligned16(halo_next);
-  const ColSplit cs = split_cols(P, vec_ok);
-  const int pf = env_int("DOL_RING_PF", 4);
-  const int nt = env_int("DOL_RING_NT", 2);
-  if (cs.n4 > 0) {
-    const int64_t nct = cdiv(cs.n4, kThreads);
-    if (env_int("DOL_RING_DMA", 1) != 0) {
-      constexpr int R = 4;
-      if (nct * cdiv(n_rows, R) > kMaxBlocks) return fail(DOL_EINVAL, "dol_mix_ring_f32: problem too large for one launch");
-      hipLaunchKernelGGL((ring_mix_dma_kernel<R>), dim3(static_cast<unsigned>(nct * cdiv(n_rows, R))), dim3(kThreads), 0, s,
-                         X, ldx, Y, ldy, n_rows, cs.n4, nct, halo_prev, halo_next, w_prev, w_next);
-    } else {
-      const int rpb = ring_rows_per_block(n_rows, nct, pf);
-      if (nct * cdiv(n_rows, rpb) > kMaxBlocks)
-        return fail(DOL_EINVAL, "dol_mix_ring_f32: problem too large for one launch");
-      launch_ring_variant<f4>(pf, nt, X, ldx, Y, ldy, n_rows, 0, cs.n4, rpb, halo_prev, halo_next, w_prev, w_next, s);
-    }
+  if (mode == 0) return mk(integral_constant<int, 1>{}, integral_constant<int, 0>{});
+  if (mode == 1) return mk(integral_constant<int, 1>{}, integral_constant<int, 1>{});
+  return mk(integral_constant<int, 1>{}, integral_constant<int, 2>{});
+}
+}  // namespace
+
+extern "C" {
+
+int dol_dgd_ring_f32(const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t n_rows, int64_t P,
+                     const float* halo_prev, const float* halo_next, const float* w_prev, const float* w_next,
+                     const float* target, int64_t ldt, float* mom, int64_t ldm, int32_t objective,
+                     int32_t local_steps, float lr, float momentum, int first_step, hipStream_t s) {
+  const char* nm = "dol_dgd_ring_f32";
+  const DgdArgs d{target, ldt, mom, ldm, objective, local_steps, lr, momentum, first_step};
+  bool evec = false;
+  int mode = 0;
+  if (n_rows > 0 && P > 0) {
+    const int rc = check_dgd(nm, d, P, &evec, &mode);
+    if (rc) return rc;
   }
-  if (cs.tail > 0) {
-    const int rpb = ring_rows_per_block(n_rows, cdiv(cs.tail, kThreads), 4);
-    if (cdiv(cs.tail, kThreads) * cdiv(n_rows, rpb) > kMaxBlocks)
-      return fail(DOL_EINVAL, "dol_mix_ring_f32: problem too large for one launch");
-    launch_ring<float, 4, false, true>(X, ldx, Y, ldy, n_rows, cs.n4 * 4, cs.tail, rpb, halo_prev, halo_next,
-                                       w_prev, w_next, s);
+  return with_dgd_epi(d, mode, [&](auto epi) {
+    return mix_ring_impl(nm, X, ldx, Y, ldy, n_rows, P, halo_prev, halo_next, w_prev, w_next, epi, evec, s);
+  });
+}
+
+int dol_dgd_csr_f32(const float* X, int64_t ldx, int32_t x_rows, float* Y, int64_t ldy, int32_t n_rows, int64_t P,
+                    const int32_t* rowptr, const int32_t* col, const float* val, const float* target, int64_t ldt,
+                    float* mom, int64_t ldm, int32_t objective, int32_t local_steps, float lr, float momentum,
+                    int first_step, hipStream_t s) {
+  const char* nm = "dol_dgd_csr_f32";
+  const DgdArgs d{target, ldt, mom, ldm, objective, local_steps, lr, momentum, first_step};
+  bool evec = false;
+  int mode = 0;
+  if (n_rows > 0 && P > 0) {
+    const int rc = check_dgd(nm, d, P, &evec, &mode);
+    if (rc) return rc;
   }
-  return check_launch("dol_mix_ring_f32");
+  return with_dgd_epi(d, mode, [&](auto epi) {
+    return mix_csr_impl(nm, X, ldx, x_rows, Y, ldy, n_rows, P, rowptr, col, val, epi, evec, s);
+  });
 }
 
 int dol_mix_dense_f32(const float* W, int64_t ldw, const float* X, int64_t ldx, float* Y, int64_t ldy,

@@ -48,6 +48,10 @@ SIGNATURES = {
     "dol_mlp_step_f32": [_ptr, _i64, _ptr, _i64, _ptr, _i64, _ptr, _ptr, _i64, _ptr, _i64, _i64, _ptr, _i64, _ptr,
                          _i32, _i32, _i32, _i32, _i32, _f32, _f32, _f32, ctypes.c_int, ctypes.c_int, _ptr, _ptr],
     "dol_mlp_step_workspace_bytes": [_i32, _i32, _i32],
+    "dol_dgd_ring_f32": [_ptr, _i64, _ptr, _i64, _i32, _i64, _ptr, _ptr, _ptr, _ptr, _ptr, _i64, _ptr, _i64, _i32, _i32,
+                         _f32, _f32, ctypes.c_int, _ptr],
+    "dol_dgd_csr_f32": [_ptr, _i64, _i32, _ptr, _i64, _i32, _i64, _ptr, _ptr, _ptr, _ptr, _i64, _ptr, _i64, _i32, _i32,
+                        _f32, _f32, ctypes.c_int, _ptr],
     "dol_mlp_step_lds_bytes": [_i32, _i32, _i32],
 }
 _RESTYPES = {"dol_last_error": ctypes.c_char_p, "dol_admm_dual_workspace_bytes": ctypes.c_int64,

@@ -341,5 +341,18 @@ class MixingPlan:
         return ops.mix_csr(X, Y, self.rowptr, self.col, self.val, P=P)
 
 
+    def apply_dgd(self, X: torch.Tensor, Y: torch.Tensor, target: torch.Tensor, mom: Optional[torch.Tensor] = None,
+                  objective: str = "least_squares", steps: int = 1, lr: float = 0.01, momentum: float = 0.0,
+                  first_step: bool = False, P: Optional[int] = None) -> torch.Tensor:
+        """One fused DGD round (mix + local steps, BASELINE config 3); ring or CSR."""
+        from . import ops
+        kw = dict(mom=mom, objective=objective, steps=steps, lr=lr, momentum=momentum, first_step=first_step, P=P)
+        if self.kind == "ring":
+            return ops.dgd_ring(X, Y, self.w_prev, self.w_next, target, n_rows=self.n_rows, **kw)
+        if self.kind == "dense":
+            raise NotImplementedError("DGD rounds are fused into the sparse mixes; use a ring/CSR plan")
+        return ops.dgd_csr(X, Y, self.rowptr, self.col, self.val, target, **kw)
+
+
 def plans_for(graphs: Sequence[Graph], device, allow_ring: bool = True) -> List[MixingPlan]:
     return [MixingPlan.from_graph(g, device, allow_ring) for g in graphs]

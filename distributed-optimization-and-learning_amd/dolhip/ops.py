@@ -16,6 +16,7 @@ from ._native import DolNativeError
 __all__ = [
     "DolNativeError", "mix_csr", "mix_ring", "mix_dense", "mix_ring_steps", "prox_admm_sgd", "admm_dual", "ordered_mean",
     "ordered_sum", "stream_copy", "dual_workspace_bytes", "prox_grad", "admm_step_dual", "mlp_step",
+    "dgd_ring", "dgd_csr", "OBJECTIVES",
 ]
 
 
@@ -93,6 +94,83 @@ def mix_ring_steps(X: torch.Tensor, Y: torch.Tensor, w_prev: torch.Tensor, w_nex
         raise ValueError("X and Y alias")
     _native.call("dol_mix_ring_steps_f32", X.data_ptr(), ldx, Y.data_ptr(), ldy, n, P, int(steps),
                  w_prev.data_ptr(), w_next.data_ptr(), _stream(X))
+    return Y
+
+
+OBJECTIVES = {"least_squares": 0, "logistic": 1}
+
+
+def _dgd_args(X, target, mom, objective, steps, momentum, P, n):
+    if objective not in OBJECTIVES:
+        raise ValueError(f"objective must be one of {sorted(OBJECTIVES)}")
+    if int(steps) < 1:
+        raise ValueError("local steps must be >= 1")
+    ldt = _check_rows("target", target, P)
+    if target.shape[0] < n or target.device != X.device:
+        raise ValueError(f"target: expected >= {n} rows on {X.device}")
+    ldm = 0
+    if momentum != 0.0:
+        if mom is None:
+            raise ValueError("momentum != 0 needs mom")
+        ldm = _check_rows("mom", mom, P)
+        if mom.shape[0] < n or mom.device != X.device:
+            raise ValueError(f"mom: expected >= {n} rows on {X.device}")
+    return ldt, ldm
+
+
+def dgd_ring(X: torch.Tensor, Y: torch.Tensor, w_prev: torch.Tensor, w_next: torch.Tensor, target: torch.Tensor,
+             mom: Optional[torch.Tensor] = None, objective: str = "least_squares", steps: int = 1, lr: float = 0.01,
+             momentum: float = 0.0, first_step: bool = False, halo_prev: Optional[torch.Tensor] = None,
+             halo_next: Optional[torch.Tensor] = None, P: Optional[int] = None,
+             n_rows: Optional[int] = None) -> torch.Tensor:
+    """One fused DGD round on a ring: Y = W X (bit-exact mix), then `steps` local
+    momentum-SGD iterations per row on a separable loss (BASELINE config 3;
+    round order of DIST/simulators.py:147-162)."""
+    P = X.shape[1] if P is None else P
+    n = X.shape[0] if n_rows is None else n_rows
+    ldx = _check_rows("X", X, P)
+    ldy = _check_rows("Y", Y, P)
+    if X.shape[0] < n or Y.shape[0] < n:
+        raise ValueError("X/Y have fewer rows than n_rows")
+    for nm, t in (("w_prev", w_prev), ("w_next", w_next)):
+        if t.device != X.device or t.dtype != torch.float32 or t.numel() < n or not t.is_contiguous():
+            raise ValueError(f"{nm}: expected contiguous float32 [{n}] on {X.device}")
+    if (halo_prev is None) != (halo_next is None):
+        raise ValueError("pass both halos or neither")
+    if halo_prev is None and n < 3:
+        raise ValueError("a wrap-around ring needs >= 3 rows (use dgd_csr)")
+    _check_vec("halo_prev", halo_prev, P, X.device)
+    _check_vec("halo_next", halo_next, P, X.device)
+    if X.data_ptr() == Y.data_ptr():
+        raise ValueError("X and Y alias: the Jacobi mix needs two buffers")
+    ldt, ldm = _dgd_args(X, target, mom, objective, steps, momentum, P, n)
+    _native.call("dol_dgd_ring_f32", X.data_ptr(), ldx, Y.data_ptr(), ldy, n, P, _ptr(halo_prev), _ptr(halo_next),
+                 w_prev.data_ptr(), w_next.data_ptr(), target.data_ptr(), ldt, _ptr(mom) if ldm else None, ldm,
+                 OBJECTIVES[objective], int(steps), float(lr), float(momentum), int(bool(first_step)), _stream(X))
+    return Y
+
+
+def dgd_csr(X: torch.Tensor, Y: torch.Tensor, rowptr: torch.Tensor, col: torch.Tensor, val: torch.Tensor,
+            target: torch.Tensor, mom: Optional[torch.Tensor] = None, objective: str = "least_squares",
+            steps: int = 1, lr: float = 0.01, momentum: float = 0.0, first_step: bool = False,
+            P: Optional[int] = None) -> torch.Tensor:
+    """dgd_ring for any W (CSR mix, bit-exact), then the same local steps."""
+    P = X.shape[1] if P is None else P
+    ldx = _check_rows("X", X, P)
+    ldy = _check_rows("Y", Y, P)
+    n = rowptr.shape[0] - 1
+    if Y.shape[0] < n:
+        raise ValueError(f"Y has {Y.shape[0]} rows < {n}")
+    for nm, t, dt in (("rowptr", rowptr, torch.int32), ("col", col, torch.int32), ("val", val, torch.float32)):
+        if t.device != X.device or t.dtype != dt or not t.is_contiguous():
+            raise ValueError(f"{nm}: expected contiguous {dt} on {X.device}")
+    if X.data_ptr() == Y.data_ptr():
+        raise ValueError("X and Y alias: the Jacobi mix needs two buffers")
+    ldt, ldm = _dgd_args(X, target, mom, objective, steps, momentum, P, n)
+    _native.call("dol_dgd_csr_f32", X.data_ptr(), ldx, X.shape[0], Y.data_ptr(), ldy, n, P, rowptr.data_ptr(),
+                 col.data_ptr() if col.numel() else None, val.data_ptr() if val.numel() else None,
+                 target.data_ptr(), ldt, _ptr(mom) if ldm else None, ldm, OBJECTIVES[objective], int(steps),
+                 float(lr), float(momentum), int(bool(first_step)), _stream(X))
     return Y
 
 

@@ -104,6 +104,29 @@ int dol_mix_dense_f32(const float* W, int64_t ldw, const float* X, int64_t ldx,
                       hipStream_t s);
 
 /*
+ * One round of decentralised gradient descent on a separable synthetic loss
+ * (BASELINE config 3), fused: the gossip mix of dol_mix_ring_f32 /
+ * dol_mix_csr_f32 (same arguments, same bit-exact mix), then `local_steps`
+ * momentum-SGD iterations per agent in the reference's round order
+ * (DIST/simulators.py:147-162: consensus, then local_update with
+ * torch.optim.SGD(lr, momentum), DIST/clients.py:17,43-49):
+ *   objective 0, least squares f_i(x) = 1/2 ||x - t_i||^2:     g = fl(x - t)
+ *   objective 1, logistic (diagonal features, t = label*feature):
+ *                f_i(x) = sum_p log(1 + exp(-t_p x_p)):         g = -t / (1 + exp(t x))
+ *   buf = (first_step && s == 0) ? g : fl(fl(buf*momentum) + g);  x = fma(-lr, buf or g, x)
+ * target: rows aligned with Y (ldt); mom: momentum rows (ldm), NULL iff momentum == 0.
+ * One pass streams X (and the neighbours), the targets and the momentum once.
+ */
+int dol_dgd_ring_f32(const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t n_rows, int64_t P,
+                     const float* halo_prev, const float* halo_next, const float* w_prev, const float* w_next,
+                     const float* target, int64_t ldt, float* mom, int64_t ldm, int32_t objective,
+                     int32_t local_steps, float lr, float momentum, int first_step, hipStream_t s);
+int dol_dgd_csr_f32(const float* X, int64_t ldx, int32_t x_rows, float* Y, int64_t ldy, int32_t n_rows, int64_t P,
+                    const int32_t* rowptr, const int32_t* col, const float* val, const float* target, int64_t ldt,
+                    float* mom, int64_t ldm, int32_t objective, int32_t local_steps, float lr, float momentum,
+                    int first_step, hipStream_t s);
+
+/*
  * Fused local step of n_agents agents (rows of w/buf/g), replacing:
  *   FedProx_Client.update_model  DEC/clients.py:101-115  g' = fl(g + fl(rho*fl(w-theta)))
  *   FedAdmm_Client.update_model  DEC/clients.py:125-139  g' = fl(g + fl(alpha + fl(rho*fl(w-theta))))

@@ -50,6 +50,9 @@ def lib():
         L.oracle_admm_dual_f32.argtypes = [_f32p, _i64, _f32p, _i64, _f32p, ctypes.c_float, _i32, _i64, _f64p]
         L.oracle_ordered_mean_f32.argtypes = [_f32p, _i64, _i32p, _i32, _i64, _f32p]
         L.oracle_ordered_sum_f32.argtypes = [_f32p, _i64, _i32p, _i32, _i64, _f32p, _f32p, ctypes.c_float]
+        L.oracle_dgd_local_f32.argtypes = [_f32p, _i64, _f32p, _i64, _f32p, _i64, _i32, _i64, _i32, _i32,
+                                           ctypes.c_float, ctypes.c_float, ctypes.c_int]
+        L.oracle_dgd_local_f32.restype = None
         for f in (L.oracle_mix_csr_f32, L.oracle_mix_ring_f32, L.oracle_prox_admm_sgd_f32,
                   L.oracle_admm_dual_f32, L.oracle_ordered_mean_f32, L.oracle_ordered_sum_f32):
             f.restype = None
@@ -137,6 +140,20 @@ def ordered_sum(W, order, acc_in=None, scale=1.0):
     ai = None if acc_in is None else _f32c(acc_in)
     lib().oracle_ordered_sum_f32(_p(W), P, _p(order, _i32p), len(order), P, _p(ai), _p(out), scale)
     return out
+
+
+OBJECTIVES = {"least_squares": 0, "logistic": 1}
+
+
+def dgd_local(Y, T, M, objective, steps, lr, momentum, first_step):
+    """Local steps after the mix (config 3); returns (Y', M') (M' None without momentum)."""
+    Y = _f32c(Y).copy()
+    T = _f32c(T)
+    n, P = Y.shape
+    M = None if M is None else _f32c(M).copy()
+    lib().oracle_dgd_local_f32(_p(Y), P, _p(T), P, _p(M), P, n, P, OBJECTIVES[objective], int(steps), lr,
+                               momentum, int(first_step))
+    return Y, M
 
 
 def bits_equal(a, b):

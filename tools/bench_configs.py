@@ -99,6 +99,37 @@ def mlp_round(N, d, h, c, B, p_edge, reps, dev):
     torch.cuda.empty_cache()
 
 
+def dgd_round(N, P, topo, objective, momentum, steps, reps, dev):
+    """BASELINE config 3: one fused DGD round (mix + local momentum-SGD steps on a
+    separable synthetic loss) over all agents; algorithmic bytes = N*P*4 *
+    (x read + y write + target read [+ momentum read + write])."""
+    from dolhip.synthetic import SeparableDGD
+    if topo == "ring":
+        torch.manual_seed(2028)
+        plan = G.MixingPlan(G.communication_csr("circle", "stochastic", N)[0], dev)
+    else:
+        plan = G.MixingPlan(G.random_regular_csr(N, int(topo[2:]), seed=2028), dev)
+    prob = SeparableDGD(plan, P, objective=objective, lr=0.01, momentum=momentum, local_steps=steps, seed=7)
+    for _ in range(2):
+        prob.round()
+    torch.cuda.synchronize()
+    s_, e_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s_.record()
+    for _ in range(reps):
+        prob.round()
+    e_.record()
+    torch.cuda.synchronize()
+    ms = s_.elapsed_time(e_) / reps
+    alg = N * P * 4 * (3 + (2 if momentum else 0))
+    print(json.dumps({"workload": "config3: fused DGD round (mix + %d local step%s)" % (steps, "s" * (steps > 1)),
+                      "topology": topo, "kernel": plan.kind, "objective": objective, "momentum": momentum,
+                      "agents": N, "params": P, "ms_per_round": ms, "rounds_per_s": 1e3 / ms,
+                      "algorithmic_bytes": alg, "GBps": alg / (ms / 1e3) / 1e9,
+                      "frac_of_8TBps": alg / (ms / 1e3) / 1e9 / 8000.0}), flush=True)
+    del prob, plan
+    torch.cuda.empty_cache()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--agents", type=int, nargs="*", default=[1024, 8192])
@@ -107,11 +138,17 @@ def main():
     ap.add_argument("--topologies", nargs="+", default=["ring", "ring-eps5", "rr4", "dense-er0.1"])
     ap.add_argument("--dense-max-agents", type=int, default=2048)
     ap.add_argument("--mlp", type=int, nargs="*", default=[1024], help="agent counts for the config-5 MLP round")
+    ap.add_argument("--dgd", type=int, nargs="*", default=[1024], help="agent counts for the config-3 DGD round")
+    ap.add_argument("--dgd-topologies", nargs="+", default=["ring", "rr4"])
     a = ap.parse_args()
     dev = torch.device("cuda")
     P = a.params
     for N in a.mlp:
         mlp_round(N, 784, 128, 10, 32, 0.1, a.reps, dev)
+    for N in a.dgd:
+        for topo in a.dgd_topologies:
+            dgd_round(N, P, topo, "least_squares", 0.5, 1, a.reps, dev)
+            dgd_round(N, P, topo, "logistic", 0.0, 1, a.reps, dev)
     for N in a.agents:
         ld = row_stride(P)
         X = torch.empty(N, ld, device=dev).normal_()
