@@ -10,6 +10,13 @@ contiguous blocks, one block per rank:
   (send/recv over RCCL/xGMI, or gloo on CPU), then the two boundary rows are
   mixed.  Results are bit-identical to the single-GPU mix for every world size
   (each output row sees the same two products added in the same order).
+* parameter-dimension sharding (ColumnSharded): for graphs whose
+  edges are not local in agent order (random-regular, Erdős–Rényi, dense W)
+  an agent block would need most of X from other ranks every round; instead
+  each rank owns ALL agents x a contiguous block of parameter columns, and
+  Y[:, cols] = W X[:, cols] (also the fused config-3 DGD round, whose local
+  steps are per-coordinate) needs no communication at all.  Bit-identical to
+  one GPU: every column's arithmetic is unchanged.
 * global mean (FedAvg / FedProx / FedADMM server average): each rank sums its
   local sampled rows in sampled order, then `all_reduce(SUM)` and a division
   by m ("fast", association order differs from the reference by rank), or an
@@ -129,6 +136,74 @@ class ShardedRing:
                       halo_prev=x[n - 2], halo_next=self.halo_next, P=P, n_rows=1)
         if own:
             self.x, self.y = self.y, self.x
+
+
+def column_bounds(P: int, world: int, rank: int, align: int = 64) -> Tuple[int, int]:
+    """Contiguous block [c0, c1) of the parameter dimension owned by `rank`, cut
+    on multiples of `align` floats (16-B lanes, whole 256-B tiles)."""
+    units = (P + align - 1) // align
+    lo, hi = shard_bounds(units, world, rank)
+    return min(lo * align, P), min(hi * align, P)
+
+
+class ColumnSharded:
+    """Mixing with ANY W sharded over the parameter dimension (one process per
+    GPU).  x / y: local [N, ld] buffers holding columns [c0, c1) of every agent.
+    `step()` = one Jacobi round; `dgd_step()` = one fused config-3 round with
+    the local `target` / `mom` blocks.  No collective on the data path."""
+
+    def __init__(self, plan, P: int, device, group=None, alloc: bool = True, apply=None, apply_dgd=None):
+        # apply / apply_dgd: kernel entries (default: the plan's HIP ops); tests inject a CPU checker
+        self.plan = plan
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.N, self.P = plan.n_rows, P
+        self.c0, self.c1 = column_bounds(P, self.world, self.rank)
+        self.Pl = self.c1 - self.c0
+        self.device = torch.device(device)
+        self.ld = row_stride(max(self.Pl, 1))
+        self._apply = apply if apply is not None else plan.apply
+        self._apply_dgd = apply_dgd if apply_dgd is not None else plan.apply_dgd
+        if alloc:
+            self.x = torch.empty(self.N, self.ld, dtype=torch.float32, device=self.device)
+            self.y = torch.empty_like(self.x)
+
+    def local_cols(self, full: torch.Tensor) -> torch.Tensor:
+        """This rank's column block of a full [N, >=P] matrix."""
+        return full[:, self.c0:self.c1]
+
+    def step(self) -> None:
+        if self.Pl > 0:
+            self._apply(self.x, self.y, P=self.Pl)
+        self.x, self.y = self.y, self.x
+
+    def dgd_step(self, target: torch.Tensor, mom: Optional[torch.Tensor] = None, **kw) -> None:
+        if self.Pl > 0:
+            self._apply_dgd(self.x, self.y, target, mom=mom, P=self.Pl, **kw)
+        self.x, self.y = self.y, self.x
+
+    def gather(self, dst: int = 0) -> Optional[torch.Tensor]:
+        """Full [N, P] on rank `dst` (checkpoints / tests; not on the round path)."""
+        mine = self.x[:, :self.Pl].contiguous()
+        if self.world == 1:
+            return mine
+        staged = mine.device.type == "cuda" and dist.get_backend(self.group) == "gloo"
+        send = mine.cpu() if staged else mine
+        if self.rank != dst:
+            if self.Pl > 0:
+                dist.send(send, dst=dst, group=self.group)
+            return None
+        parts = []
+        for r in range(self.world):
+            a, b = column_bounds(self.P, self.world, r)
+            if r == self.rank:
+                parts.append(send)
+            elif b > a:  # uneven blocks: point-to-point with known shapes
+                t = torch.empty(self.N, b - a, dtype=torch.float32, device=send.device)
+                dist.recv(t, src=r, group=self.group)
+                parts.append(t)
+        return torch.cat(parts, dim=1)
 
 
 def global_mean(local_rows: torch.Tensor, local_order: Sequence[int], m_total: int, P: int,

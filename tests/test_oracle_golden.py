@@ -87,3 +87,25 @@ def test_ordered_mean_matches_reference_average_weights(name):
         part = oracle.ordered_sum(W, np.arange(2))
         full = oracle.ordered_sum(W, np.arange(2, m), acc_in=part, scale=float(m))
         assert bits_equal(full, A[name + "__theta"])
+
+
+@pytest.mark.parametrize("momentum,first", [(0.0, False), (0.5, True), (0.5, False)])
+def test_dgd_local_step_is_the_pinned_sgd_step(momentum, first):
+    """Config 3's local step (oracle_dgd_local_f32, least squares) is the
+    reference-pinned SGD update above (oracle_prox_admm_sgd_f32, no prox term)
+    applied to g = fl(x - t) — which is exactly what torch autograd returns for
+    0.5 * sum((x - t)**2) (the *2 and *0.5 scalings are exact)."""
+    import torch
+    rng = np.random.default_rng(3)
+    Y = rng.standard_normal((4, 301)).astype(np.float32)
+    T = rng.standard_normal((4, 301)).astype(np.float32)
+    M = rng.standard_normal((4, 301)).astype(np.float32)
+    x = torch.from_numpy(Y.copy()).requires_grad_(True)
+    (0.5 * ((x - torch.from_numpy(T)) ** 2).sum()).backward()
+    g = (Y - T).astype(np.float32)
+    assert bits_equal(x.grad.numpy(), g)
+    got_y, got_m = oracle.dgd_local(Y, T, M if momentum else None, "least_squares", 1, 0.05, momentum, first)
+    want_w, want_b, _ = oracle.prox_admm_sgd(Y, M if momentum else None, g, None, None, 0.0, 0.05, momentum, first)
+    assert bits_equal(got_y, want_w)
+    if momentum:
+        assert bits_equal(got_m, want_b)

@@ -97,3 +97,75 @@ def test_sharded_ring_and_means_match_single_process(world, N):
     for r in res:
         assert oracle.bits_equal(r[4], want_mean)  # exact chain: bit-identical on every rank
         np.testing.assert_allclose(r[5], want_mean, rtol=1e-5, atol=1e-6)  # all_reduce form
+
+
+def cpu_apply_csr(csr):
+    def apply(X, Y, P=None):
+        Y[:, :P] = torch.from_numpy(oracle.mix_csr(X[:, :P].numpy(), csr.rowptr, csr.col, csr.val))
+        return Y
+    return apply
+
+
+def cpu_apply_dgd(csr):
+    def apply_dgd(X, Y, target, mom=None, objective="least_squares", steps=1, lr=0.01, momentum=0.0,
+                  first_step=False, P=None):
+        mixed = oracle.mix_csr(X[:, :P].numpy(), csr.rowptr, csr.col, csr.val)
+        y, m = oracle.dgd_local(mixed, target[:, :P].numpy(), None if mom is None else mom[:, :P].numpy(),
+                                objective, steps, lr, momentum, first_step)
+        Y[:, :P] = torch.from_numpy(y)
+        if mom is not None and m is not None:
+            mom[:, :P] = torch.from_numpy(m)
+        return Y
+    return apply_dgd
+
+
+def _column_worker(rank, world, port, N, P, rounds, q):
+    from dolhip import graph as G
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        csr = G.random_regular_csr(N, 4, seed=5)
+        plan = type("Plan", (), {"n_rows": N})()  # host stand-in: the arithmetic is injected
+        rng = np.random.default_rng(8)
+        X = rng.standard_normal((N, P)).astype(np.float32)
+        T = rng.standard_normal((N, P)).astype(np.float32)
+        sh = parallel.ColumnSharded(plan, P, "cpu", apply=cpu_apply_csr(csr), apply_dgd=cpu_apply_dgd(csr))
+        sh.x[:, :sh.Pl] = torch.from_numpy(X[:, sh.c0:sh.c1])
+        t_loc = torch.from_numpy(np.ascontiguousarray(T[:, sh.c0:sh.c1]))
+        m_loc = torch.zeros(N, sh.Pl)
+        for k in range(rounds):
+            sh.step()
+            sh.dgd_step(t_loc, mom=m_loc, steps=2, lr=0.1, momentum=0.5, first_step=(k == 0))
+        full = sh.gather(0)
+        q.put((rank, None if full is None else full.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,P", [(2, 300), (3, 130), (4, 100)])
+def test_column_sharded_mix_and_dgd_match_single_process(world, P):
+    """Parameter-dimension sharding: no data-path communication,
+    gathered result bit-identical to one process (incl. ranks with no columns)."""
+    from dolhip import graph as G
+    N, rounds = 24, 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_column_worker, args=(r, world, port, N, P, rounds, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    csr = G.random_regular_csr(N, 4, seed=5)
+    rng = np.random.default_rng(8)
+    X = rng.standard_normal((N, P)).astype(np.float32)
+    T = rng.standard_normal((N, P)).astype(np.float32)
+    M = np.zeros((N, P), np.float32)
+    for k in range(rounds):
+        X = oracle.mix_csr(X, csr.rowptr, csr.col, csr.val)
+        X, M = oracle.dgd_local(oracle.mix_csr(X, csr.rowptr, csr.col, csr.val), T, M, "least_squares", 2, 0.1,
+                                0.5, k == 0)
+    assert oracle.bits_equal(res[0], X)

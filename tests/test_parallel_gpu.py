@@ -76,3 +76,60 @@ def test_sharded_ring_real_kernels_on_one_gpu(world, N):
     for r in res:
         assert oracle.bits_equal(r[2], want)
         np.testing.assert_allclose(r[3], want, rtol=1e-5, atol=1e-6)
+
+
+def _column_worker(rank, world, port, N, P, rounds, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "distributed-optimization-and-learning_amd"))
+    from dolhip import graph as G, parallel
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = torch.device("cuda:0")
+        plan = G.MixingPlan(G.random_regular_csr(N, 4, seed=6), dev)
+        rng = np.random.default_rng(9)
+        X = rng.standard_normal((N, P)).astype(np.float32)
+        T = rng.standard_normal((N, P)).astype(np.float32)
+        sh = parallel.ColumnSharded(plan, P, dev)
+        sh.x[:, :sh.Pl] = torch.from_numpy(X[:, sh.c0:sh.c1]).to(dev)
+        t_loc = torch.from_numpy(np.ascontiguousarray(T[:, sh.c0:sh.c1])).to(dev)
+        m_loc = torch.zeros(N, sh.Pl, device=dev)
+        for k in range(rounds):
+            sh.step()
+            sh.dgd_step(t_loc, mom=m_loc, steps=2, lr=0.1, momentum=0.5, first_step=(k == 0))
+        full = sh.gather(0)
+        torch.cuda.synchronize()
+        q.put((rank, None if full is None else full.cpu().numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,N,P", [(2, 600, 4096 + 64), (3, 40, 1000)])
+def test_column_sharded_real_kernels_on_one_gpu(world, N, P):
+    """Parameter-dimension sharding with the HIP CSR + DGD kernels: gathered
+    result bit-identical to the single-process oracle."""
+    import oracle
+    from dolhip import graph as G
+    rounds = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_column_worker, args=(r, world, port, N, P, rounds, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    csr = G.random_regular_csr(N, 4, seed=6)
+    rng = np.random.default_rng(9)
+    X = rng.standard_normal((N, P)).astype(np.float32)
+    T = rng.standard_normal((N, P)).astype(np.float32)
+    M = np.zeros((N, P), np.float32)
+    for k in range(rounds):
+        X = oracle.mix_csr(X, csr.rowptr, csr.col, csr.val)
+        X, M = oracle.dgd_local(oracle.mix_csr(X, csr.rowptr, csr.col, csr.val), T, M, "least_squares", 2, 0.1,
+                                0.5, k == 0)
+    assert oracle.bits_equal(res[0], X)
