@@ -291,7 +291,7 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "ring_mix_dma_kernel<4>" if os.environ.get("DOL_RING_DMA", "1") != "0" else "ring_mix_kernel",
+                "kernel": "ring_mix_dma_kernel<4, NoEpi>" if os.environ.get("DOL_RING_DMA", "1") != "0" else "ring_mix_kernel",
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",

@@ -18,6 +18,7 @@ def rows(path):
 
 
 def short(name):
+    name = name.replace("(anonymous namespace)::", "")
     m = re.search(r"(\w+_kernel)(<[^(]*>)?", name)
     if m:
         return m.group(1) + (m.group(2) or "")
