@@ -287,6 +287,24 @@ def random_regular_csr(n: int, degree: int = 4, seed: int = 2028) -> CSR:
     return CSR(n, n, rowptr.astype(np.int32), cols_w.astype(np.int32), vals_w)
 
 
+def erdos_renyi_stochastic(n: int, p: float, generator: torch.Generator, device=None) -> torch.Tensor:
+    """Dense W of a seeded undirected Erdős–Rényi G(n, p) graph under the
+    reference's 'stochastic' weighting (DIST/simulators.py:65-70: G = R o A,
+    G /= colsum(G), W = G^T), built on the generator's device (no host round
+    trip, so a new W every round is cheap: BASELINE config 5's time-varying
+    dense W; not a reference topology).  Zero diagonal like every reference
+    adjacency; entries Neighbors would drop (NaN from an empty column, <= 0)
+    are 0, so the dense MFMA mix equals the CSR selection."""
+    dev = generator.device if device is None else torch.device(device)
+    up = torch.rand(n, n, generator=generator, device=dev) < p
+    A = torch.triu(up, diagonal=1)
+    A = (A | A.T).to(torch.float32)
+    g = torch.rand(n, n, generator=generator, device=dev) * A
+    g = g / g.sum(0)
+    W = g.T.contiguous()
+    return torch.where(W > 0, W, torch.zeros((), dtype=W.dtype, device=dev))
+
+
 class MixingPlan:
     """Device form of one W: CSR tensors plus the ring specialisation if it applies."""
 
@@ -310,7 +328,23 @@ class MixingPlan:
 
     @property
     def density(self) -> float:
+        if self.csr is None:
+            return float((self.W > 0).sum().item()) / max(1, self.W.numel())
         return self.csr.nnz / max(1, self.csr.n_rows * self.csr.n_cols)
+
+    @classmethod
+    def from_dense(cls, W: torch.Tensor) -> "MixingPlan":
+        """A 'dense' plan straight from a device W (no CSR; e.g. a per-round
+        erdos_renyi_stochastic draw).  Only apply() (fp32 MFMA) is available."""
+        if W.device.type != "cuda" or W.dtype != torch.float32 or W.dim() != 2:
+            raise ValueError("from_dense: expected a 2-D float32 CUDA tensor")
+        plan = cls.__new__(cls)
+        plan.csr = None
+        plan.device = W.device
+        plan.n_rows = W.shape[0]
+        plan.kind = "dense"
+        plan.W = W.contiguous()
+        return plan
 
     @classmethod
     def from_graph(cls, W: Graph, device, allow_ring: bool = True, dense: bool = False) -> "MixingPlan":

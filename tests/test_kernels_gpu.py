@@ -401,3 +401,27 @@ def test_admm_step_dual_equals_two_calls(mom, first, extra, gpu):
     assert bits_equal(gd[:, :P].cpu().numpy(), g1)
     if mom != 0:
         assert bits_equal(bd[:, :P].cpu().numpy(), b1)
+
+
+def test_erdos_renyi_device_plan_within_gamma_bound(gpu):
+    """Config 5's per-round W: undirected ER support (symmetric, zero diagonal),
+    the reference's 'stochastic' weighting (rows of W sum to 1), and the dense
+    MFMA mix of it within the fp32 fma-chain bound of the bit-exact CSR mix."""
+    n, P = 300, 1031
+    gen = torch.Generator(device=gpu).manual_seed(5)
+    W = G.erdos_renyi_stochastic(n, 0.1, gen)
+    Wc = W.cpu().numpy()
+    assert np.all(np.diag(Wc) == 0)
+    assert np.array_equal(Wc > 0, (Wc > 0).T)
+    nz = (Wc > 0).any(1)
+    np.testing.assert_allclose(Wc[nz].astype(np.float64).sum(1), 1.0, rtol=1e-5)
+    plan = G.MixingPlan.from_dense(W)
+    assert plan.kind == "dense" and abs(plan.density - (Wc > 0).mean()) < 1e-12
+    rng = np.random.default_rng(6)
+    X = rng.standard_normal((n, P)).astype(np.float32)
+    Y = torch.empty(n, P, device=gpu)
+    plan.apply(dev(X, gpu), Y)
+    torch.cuda.synchronize()
+    csr = G.csr_from_dense(Wc)
+    exact = oracle.mix_csr(X, csr.rowptr, csr.col, csr.val)
+    assert np.all(np.abs(Y.cpu().numpy() - exact) <= 2 * _gamma_bound(Wc, X) + 1e-30)

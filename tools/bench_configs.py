@@ -33,7 +33,9 @@ def time_plan(plan, X, Y, P, reps):
 
 
 def mlp_round(N, d, h, c, B, p_edge, reps, dev):
-    """BASELINE config 5: Erdos-Renyi W (dense, MFMA) mixing + one batched MLP local step per round."""
+    """BASELINE config 5: a NEW Erdos-Renyi W every round (drawn on the device,
+    graph.erdos_renyi_stochastic), mixed on the dense fp32 MFMA path, then one
+    fused local step of every agent's MLP (dol_mlp_step_f32)."""
     from dolhip.bank import AgentBank
     from dolhip.mlp import BatchedMLP, mlp_layout
     bank = AgentBank(N, mlp_layout(d, h, c), dev)
@@ -41,24 +43,26 @@ def mlp_round(N, d, h, c, B, p_edge, reps, dev):
     bank.buffer("x").normal_(0, 0.05)
     bank.buffer("y").zero_()
     bank.buffer("mom", zero=True)
-    gen = torch.Generator().manual_seed(2028)
-    A = (torch.rand(N, N, generator=gen) < p_edge).float()
-    A.fill_diagonal_(0)
-    R = torch.rand(N, N, generator=gen) * A
-    R /= R.sum(0).clamp_min(1e-30)
-    plan = G.MixingPlan.from_graph(R.T.contiguous(), dev, dense=True)
+    gen = torch.Generator(device=dev).manual_seed(2028)
+    state = {}
+
+    def draw():
+        state["plan"] = G.MixingPlan.from_dense(G.erdos_renyi_stochastic(N, p_edge, gen))
     X = torch.randn(N, B, d, device=dev)
     y = torch.randint(0, c, (N, B), device=dev)
     ev = {k: [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
-          for k in ("local", "mix")}
+          for k in ("graph", "local", "mix")}
 
     def one(k=None):
         r = (lambda nm, i: ev[nm][k][i].record()) if k is not None else (lambda nm, i: None)
+        r("graph", 0)
+        draw()
+        r("graph", 1)
         r("local", 0)
         mlp.step(X, y, lr=0.05, momentum=0.5, first_step=False)   # fused fwd+CE+bwd+SGD (one kernel)
         r("local", 1)
         r("mix", 0)
-        bank.mix(plan)
+        bank.mix(state["plan"])
         r("mix", 1)
     for _ in range(2):
         one()
@@ -87,7 +91,8 @@ def mlp_round(N, d, h, c, B, p_edge, reps, dev):
     P = bank.P
     flops_fb = 2.0 * N * B * (d * h + h * c) * 3  # fwd + two backward GEMMs per layer
     local_bytes = N * (4 * P + B * d) * 4           # w, mom in + out, X in (compulsory)
-    out = {"workload": "config5: ER p=%.2f dense MFMA mix + batched MLP %d-%d-%d local step" % (p_edge, d, h, c),
+    out = {"workload": "config5: time-varying ER p=%.2f (new W per round, on device) dense MFMA mix + fused MLP "
+                       "%d-%d-%d local step" % (p_edge, d, h, c),
            "agents": N, "params": P, "batch": B, "ms_per_round": el * 1e3, "rounds_per_s": 1 / el, "kernel_ms": ms,
            "mix_TFLOPs": 2.0 * N * N * P / (ms["mix"] / 1e3) / 1e12,
            "local_TFLOPs": flops_fb / (ms["local"] / 1e3) / 1e12,
@@ -95,7 +100,7 @@ def mlp_round(N, d, h, c, B, p_edge, reps, dev):
            "local_frac_of_8TBps": local_bytes / (ms["local"] / 1e3) / 1e9 / 8000.0,
            "local_speedup_vs_unfused": ms["local_unfused"] / ms["local"]}
     print(json.dumps(out), flush=True)
-    del bank, mlp, plan, X, y
+    del bank, mlp, state, X, y
     torch.cuda.empty_cache()
 
 
