@@ -99,11 +99,21 @@ def cpu_baseline(n_agents: int, P: int, seconds: float, full_agents: int):
     # per-byte extrapolation to the metric's 8192-agent system (optimistic for
     # the reference: its O(N^2) neighbour scan grows faster than linearly)
     value = rate * n_agents / full_agents
+    # the stronger CPU bar, same sample, whole-matrix torch ops
+    rw = G.csr_from_dense(W).ring_weights()
+    vr, vsec = ref_cpu.time_vectorized(X, torch.from_numpy(rw[0]), torch.from_numpy(rw[1]), min_seconds=seconds / 3)
+    vrate = vr / vsec
+    vectorized = {"value": vrate * n_agents / full_agents, "unit": "rounds/s", "cores": threads, "kind": "port",
+                  "sample": (f"vectorized torch-CPU ring round (oracle/ref_cpu.py: roll + mul + add over the whole "
+                             f"[{n_agents}, {P}] matrix) : {vr} rounds in {vsec:.2f} s = {vrate:.3f} rounds/s = "
+                             f"{2 * n_agents * P * 4 * vrate / 1e9:.1f} GB/s; value per-byte extrapolated to "
+                             f"{full_agents} agents")}
     return {
         "value": value,
         "unit": "rounds/s",
         "cores": threads,
         "kind": "port",
+        "vectorized": vectorized,
         "sample": (f"reference-structured torch-CPU round (Neighbors scan + consensus + load_state_dict, "
                    f"oracle/ref_cpu.py) on {n_agents} agents x {P} params, circle/stochastic: {rounds} rounds "
                    f"in {sec:.2f} s = {rate:.3f} rounds/s; value = that x {n_agents}/{full_agents} "

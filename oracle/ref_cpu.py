@@ -58,3 +58,26 @@ def time_rounds(W: torch.Tensor, X: torch.Tensor, min_seconds: float = 10.0, max
         mixing_round(W, agents)
         r += 1
     return r, time.perf_counter() - t0
+
+
+def vectorized_ring_round(X: torch.Tensor, Y: torch.Tensor, w_prev: torch.Tensor, w_next: torch.Tensor) -> None:
+    """The stronger CPU bar of SURVEY §8d(2): the same ring round with whole-
+    matrix torch ops (no per-agent Python loop): Y = wp*X[i-1] + wn*X[i+1], the
+    reference's rounding order without the +0 start (equal to the loop above
+    except that a sum of two -0 products comes out -0 instead of +0).  A timing
+    baseline only; parity is checked against dol_oracle.c."""
+    torch.mul(torch.roll(X, 1, 0), w_prev[:, None], out=Y)
+    Y.add_(torch.roll(X, -1, 0).mul_(w_next[:, None]))
+
+
+def time_vectorized(X: torch.Tensor, w_prev: torch.Tensor, w_next: torch.Tensor, min_seconds: float = 5.0,
+                    max_rounds: int = 200):
+    Y = torch.empty_like(X)
+    vectorized_ring_round(X, Y, w_prev, w_next)
+    t0 = time.perf_counter()
+    r = 0
+    while r < 2 or (time.perf_counter() - t0 < min_seconds and r < max_rounds):
+        vectorized_ring_round(X, Y, w_prev, w_next)
+        X, Y = Y, X
+        r += 1
+    return r, time.perf_counter() - t0
