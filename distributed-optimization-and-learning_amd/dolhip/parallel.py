@@ -50,9 +50,10 @@ class ShardedRing:
     """
 
     def __init__(self, n_agents: int, P: int, w_prev, w_next, device, ld: Optional[int] = None,
-                 group=None, alloc: bool = True, mix_ring=None):
-        # mix_ring: kernel entry (defaults to the HIP op); tests inject a CPU checker
+                 group=None, alloc: bool = True, mix_ring=None, dgd_ring=None):
+        # mix_ring / dgd_ring: kernel entries (default: the HIP ops); tests inject CPU checkers
         self._mix = mix_ring if mix_ring is not None else ops.mix_ring
+        self._dgd = dgd_ring if dgd_ring is not None else ops.dgd_ring
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
@@ -136,6 +137,32 @@ class ShardedRing:
                       halo_prev=x[n - 2], halo_next=self.halo_next, P=P, n_rows=1)
         if own:
             self.x, self.y = self.y, self.x
+
+    def dgd_step(self, target: torch.Tensor, mom: Optional[torch.Tensor] = None, **kw) -> None:
+        """One fused config-3 round (mix + local steps, dol_dgd_ring_f32) on the
+        local block; target / mom are the LOCAL [n_local, >=P] rows.  Same halo
+        schedule as step(); bit-identical to the single-GPU round."""
+        x, y = self.x, self.y
+        n, P = self.n_local, self.P
+        m = (lambda a, b: None) if mom is None else (lambda a, b: mom[a:b])
+        if self.world == 1:
+            self._dgd(x, y, self.w_prev, self.w_next, target, mom=mom, P=P, n_rows=n, **kw)
+        else:
+            reqs = self._exchange(x)
+            if n > 2:
+                ev = self.kernel_events
+                if ev:
+                    ev[0].record()
+                self._dgd(x[1:], y[1:], self.w_prev[1:], self.w_next[1:], target[1:], mom=m(1, n - 1),
+                          halo_prev=x[0], halo_next=x[n - 1], P=P, n_rows=n - 2, **kw)
+                if ev:
+                    ev[1].record()
+            self._finish_exchange(reqs)
+            self._dgd(x[0:1], y[0:1], self.w_prev[0:1], self.w_next[0:1], target[0:1], mom=m(0, 1),
+                      halo_prev=self.halo_prev, halo_next=x[1], P=P, n_rows=1, **kw)
+            self._dgd(x[n - 1:n], y[n - 1:n], self.w_prev[n - 1:n], self.w_next[n - 1:n], target[n - 1:n],
+                      mom=m(n - 1, n), halo_prev=x[n - 2], halo_next=self.halo_next, P=P, n_rows=1, **kw)
+        self.x, self.y = self.y, self.x
 
 
 def column_bounds(P: int, world: int, rank: int, align: int = 64) -> Tuple[int, int]:

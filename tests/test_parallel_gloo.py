@@ -69,7 +69,7 @@ def _worker(rank, world, port, N, P, rounds, order, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,N", [(2, 10), (3, 11), (2, 4)])
+@pytest.mark.parametrize("world,N", [(2, 10), (3, 11), (2, 4), (8, 35)])
 def test_sharded_ring_and_means_match_single_process(world, N):
     P, rounds = 37, 3
     order = [7 % N, 0, N - 1, 3, 1, 2]
@@ -169,3 +169,65 @@ def test_column_sharded_mix_and_dgd_match_single_process(world, P):
         X, M = oracle.dgd_local(oracle.mix_csr(X, csr.rowptr, csr.col, csr.val), T, M, "least_squares", 2, 0.1,
                                 0.5, k == 0)
     assert oracle.bits_equal(res[0], X)
+
+
+def cpu_dgd_ring(X, Y, w_prev, w_next, target, mom=None, halo_prev=None, halo_next=None, P=None, n_rows=None,
+                 objective="least_squares", steps=1, lr=0.01, momentum=0.0, first_step=False):
+    n = X.shape[0] if n_rows is None else n_rows
+    hp = None if halo_prev is None else halo_prev[:P].numpy()
+    hn = None if halo_next is None else halo_next[:P].numpy()
+    mixed = oracle.mix_ring(X[:n, :P].numpy(), w_prev[:n].numpy(), w_next[:n].numpy(), hp, hn)
+    y, m = oracle.dgd_local(mixed, target[:n, :P].numpy(), None if mom is None else mom[:n, :P].numpy(),
+                            objective, steps, lr, momentum, first_step)
+    Y[:n, :P] = torch.from_numpy(y)
+    if mom is not None and m is not None:
+        mom[:n, :P] = torch.from_numpy(m)
+    return Y
+
+
+def _dgd_ring_worker(rank, world, port, N, P, rounds, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rng = np.random.default_rng(12)
+        X = rng.standard_normal((N, P)).astype(np.float32)
+        T = rng.standard_normal((N, P)).astype(np.float32)
+        wp = rng.random(N).astype(np.float32)
+        wn = rng.random(N).astype(np.float32)
+        ring = parallel.ShardedRing(N, P, wp, wn, "cpu", ld=P + 5, mix_ring=cpu_mix_ring, dgd_ring=cpu_dgd_ring)
+        ring.x[:, :P] = torch.from_numpy(X[ring.lo:ring.hi])
+        t_loc = torch.from_numpy(np.ascontiguousarray(T[ring.lo:ring.hi]))
+        m_loc = torch.zeros(ring.n_local, P)
+        for k in range(rounds):
+            ring.dgd_step(t_loc, mom=m_loc, steps=2, lr=0.1, momentum=0.5, first_step=(k == 0))
+        q.put((rank, ring.x[:, :P].numpy().copy(), m_loc.numpy().copy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,N", [(2, 10), (3, 11), (8, 40)])
+def test_sharded_dgd_ring_matches_single_process(world, N):
+    """Agent-sharded config-3 rounds over the halo exchange (up to 8 ranks, the
+    node size) are bit-identical to one process."""
+    P, rounds = 29, 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dgd_ring_worker, args=(r, world, port, N, P, rounds, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=180) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    rng = np.random.default_rng(12)
+    X = rng.standard_normal((N, P)).astype(np.float32)
+    T = rng.standard_normal((N, P)).astype(np.float32)
+    wp = rng.random(N).astype(np.float32)
+    wn = rng.random(N).astype(np.float32)
+    M = np.zeros((N, P), np.float32)
+    for k in range(rounds):
+        X, M = oracle.dgd_local(oracle.mix_ring(X, wp, wn), T, M, "least_squares", 2, 0.1, 0.5, k == 0)
+    assert oracle.bits_equal(np.concatenate([r[1] for r in res]), X)
+    assert oracle.bits_equal(np.concatenate([r[2] for r in res]), M)

@@ -133,3 +133,58 @@ def test_column_sharded_real_kernels_on_one_gpu(world, N, P):
         X, M = oracle.dgd_local(oracle.mix_csr(X, csr.rowptr, csr.col, csr.val), T, M, "least_squares", 2, 0.1,
                                 0.5, k == 0)
     assert oracle.bits_equal(res[0], X)
+
+
+def _dgd_ring_worker(rank, world, port, N, P, rounds, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "distributed-optimization-and-learning_amd"))
+    from dolhip import parallel
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = torch.device("cuda:0")
+        rng = np.random.default_rng(13)
+        X = rng.standard_normal((N, P)).astype(np.float32)
+        T = rng.standard_normal((N, P)).astype(np.float32)
+        wp = rng.random(N).astype(np.float32)
+        wn = rng.random(N).astype(np.float32)
+        ring = parallel.ShardedRing(N, P, wp, wn, dev)
+        ring.x[:, :P] = torch.from_numpy(X[ring.lo:ring.hi]).to(dev)
+        t_loc = torch.from_numpy(np.ascontiguousarray(T[ring.lo:ring.hi])).to(dev)
+        m_loc = torch.zeros(ring.n_local, P, device=dev)
+        for k in range(rounds):
+            ring.dgd_step(t_loc, mom=m_loc, steps=2, lr=0.1, momentum=0.5, first_step=(k == 0))
+        torch.cuda.synchronize()
+        q.put((rank, ring.x[:, :P].cpu().numpy(), m_loc.cpu().numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,N", [(2, 64), (3, 50)])
+def test_sharded_dgd_ring_real_kernels_on_one_gpu(world, N):
+    """Agent-sharded config-3 rounds with the HIP DGD kernel and halo pointers:
+    bit-identical to the single-process oracle."""
+    import oracle
+    P, rounds = 4096 + 12, 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dgd_ring_worker, args=(r, world, port, N, P, rounds, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    rng = np.random.default_rng(13)
+    X = rng.standard_normal((N, P)).astype(np.float32)
+    T = rng.standard_normal((N, P)).astype(np.float32)
+    wp = rng.random(N).astype(np.float32)
+    wn = rng.random(N).astype(np.float32)
+    M = np.zeros((N, P), np.float32)
+    for k in range(rounds):
+        X, M = oracle.dgd_local(oracle.mix_ring(X, wp, wn), T, M, "least_squares", 2, 0.1, 0.5, k == 0)
+    assert oracle.bits_equal(np.concatenate([r[1] for r in res]), X)
+    assert oracle.bits_equal(np.concatenate([r[2] for r in res]), M)
