@@ -104,7 +104,7 @@ def communication_graph(topology: str, mode: str, n: int, sinkhorn_max_iters: in
             rand = torch.ones(n, n) / n
         out = []
         for a in graphs:
-            g = np.array(rand * torch.tensor(a).int().float())
+            g = (rand * torch.tensor(a).int().float()).numpy().copy()
             if verbose:
                 print(g.sum(1), g.sum(0))
             out.append(torch.tensor(_sinkhorn(g, sinkhorn_max_iters, sinkhorn_tol)).T)

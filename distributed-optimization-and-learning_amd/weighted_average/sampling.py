@@ -12,5 +12,6 @@ def iid_split(dataset, args):
 
 def noniid_split(dataset, args):
     num_shards = args.shards * args.num_users
-    return _shards(np.array(dataset.targets), args.num_users, args.shards, num_shards,
+    t = dataset.targets
+    return _shards(t.numpy().copy() if hasattr(t, "numpy") else np.array(t), args.num_users, args.shards, num_shards,
                    len(dataset) // num_shards)

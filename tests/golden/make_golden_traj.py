@@ -45,7 +45,7 @@ def summary(vec):
             "sum": float(vec.astype(np.float64).sum())}
 
 
-def run_dist():
+def run_dist(cls_name="DecFedAvg", overrides=None, eps=None):
     mods = _import_project(DIST_SRC, ["utils", "sampling", "simulators"])
     U, S, sim = mods["utils"], mods["sampling"], mods["simulators"]
 
@@ -55,11 +55,27 @@ def run_dist():
         return train, test, groups
 
     sim.get_dataset = get_dataset
-    args = U.DotDict(dict(DIST_ARGS, device="cpu"))
+    args = U.DotDict(dict(DIST_ARGS, **(overrides or {}), device="cpu"))
     with contextlib.redirect_stdout(io.StringIO()):
-        s = sim.DecFedAvg(args)
-        s.run(args.rounds)
+        s = getattr(sim, cls_name)(args)
+        if eps is None:
+            s.run(args.rounds)
+        else:
+            s.run(args.rounds, eps)
     return {"history": s.history, "agents": [summary(flat(c.model.state_dict())) for c in s.clients]}
+
+
+# further gossip runs: other topologies / modes, and the other simulator classes
+# (FedLCon and Centeralized mutate args exactly as the reference does)
+DIST_VARIANTS = {
+    "DecFedAvg_star": ("DecFedAvg", {"topology": "star"}, None),
+    "DecFedAvg_compelete": ("DecFedAvg", {"topology": "compelete"}, None),
+    "DecFedAvg_dynamic": ("DecFedAvg", {"topology": "dynamic"}, None),
+    "DecFedAvg_circle_double": ("DecFedAvg", {"mode": "double_stochastic"}, None),
+    "NoConsDecFedAvg": ("NoConsDecFedAvg", {}, None),
+    "FedLCon_eps3": ("FedLCon", {}, 3),
+    "Centeralized": ("Centeralized", {}, None),
+}
 
 
 def run_dec(server_name):
@@ -91,6 +107,11 @@ def main():
            "DecFedAvg": run_dist()}
     for name in ("FedAvg_Server", "FedProx_Server", "FedAdmm_Server"):
         res[name] = run_dec(name)
+    res["dist_variants"] = {}
+    for key, (cls_name, over, eps) in DIST_VARIANTS.items():
+        r = run_dist(cls_name, over, eps)
+        r.update(cls=cls_name, overrides=over, eps=eps)
+        res["dist_variants"][key] = r
     with open(os.path.join(HERE, "trajectories.json"), "w") as f:
         json.dump(res, f)
     print("wrote trajectories.json")

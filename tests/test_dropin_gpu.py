@@ -185,3 +185,26 @@ def test_sparse_graphs_simulator_matches_dense(gpu):
         outs.append(sim.bank.rows().cpu().numpy())
         assert len(sim.Neighbors(0, sim.adjacent_matrix[0])) == 1
     assert oracle.bits_equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("key", sorted(TRAJ["dist_variants"]))
+def test_gossip_variant_trajectories_match_reference(key, gpu):
+    """Other topologies (star / complete / dynamic with its NaN rows / Sinkhorn
+    double-stochastic circle) and the other simulator classes (NoConsDecFedAvg,
+    FedLCon with the shipped single-step behaviour, Centeralized) against the
+    reference's own 2-round runs; tolerances as stated in the module docstring."""
+    ref = TRAJ["dist_variants"][key]
+    m = load_project("weighted_average", ["simulators", "utils"])
+    over = dict(ref["overrides"])
+    if ref["cls"] == "FedLCon":
+        over["reference_compat"] = True  # the shipped FedLCon: 1 user, only the first eps step applies
+    args = m["utils"].DotDict(dict(TRAJ["dist_args"], **over, device="cuda"))
+    sim = getattr(m["simulators"], ref["cls"])(args)
+    if ref["eps"] is None:
+        sim.run(args.rounds)
+    else:
+        sim.run(args.rounds, ref["eps"])
+    _check_history(sim.history, ref["history"], ("avg_test_acc",), args.synthetic_test)
+    assert len(sim.clients) == len(ref["agents"])
+    for c, r in zip(sim.clients, ref["agents"]):
+        _check_summary(_flat(c.model), r, TRAJ["stride"])
