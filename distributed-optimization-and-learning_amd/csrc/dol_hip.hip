@@ -305,11 +305,19 @@ template <int STEPS, int R>
 __global__ __launch_bounds__(kThreads) void ring_steps_kernel(
     const float* __restrict__ X, int64_t ldx, float* __restrict__ Y, int64_t ldy, int n_rows,
     int64_t ncols_v, uint32_t n_col_tiles, const float* __restrict__ wprev,
-    const float* __restrict__ wnext) {
+    const float* __restrict__ wnext, uint32_t n_row_tiles) {
   constexpr int L = R + 2 * STEPS;
+  // XCD-aware order: the dispatcher deals blocks round-robin over the 8 XCDs,
+  // so XCD x = b % 8 takes column tiles x, x + 8, ... and walks each one's row
+  // tiles in order — a tile's 2*STEPS halo rows were just loaded by its
+  // predecessor into the same L2.  (Column-tile-fastest order put vertical
+  // neighbours a residency generation apart: 385 vs 431 rounds/s at eps = 5,
+  // 8192 x 2^20.)
   const uint32_t b = blockIdx.x;
-  const uint32_t ct = b % n_col_tiles;
-  const int r0 = static_cast<int>(b / n_col_tiles) * R;
+  const uint32_t x = b & 7u, l = b >> 3;
+  const uint32_t ct = (l / n_row_tiles) * 8 + x;
+  const int r0 = static_cast<int>(l % n_row_tiles) * R;
+  if (ct >= n_col_tiles) return;
   const int64_t c = int64_t(ct) * kThreads + threadIdx.x;
   if (c >= ncols_v) return;
   auto wrap = [&](int r) { r %= n_rows; return r < 0 ? r + n_rows : r; };
@@ -1072,22 +1080,25 @@ int dol_mix_ring_steps_f32(const float* X, int64_t ldx, float* Y, int64_t ldy, i
   const uint32_t nct = static_cast<uint32_t>(cdiv(n4, kThreads));
   auto go = [&](auto steps_c, auto r_c) {
     constexpr int S = decltype(steps_c)::value, R = decltype(r_c)::value;
-    const int64_t grid = int64_t(nct) * cdiv(n_rows, R);
+    const int64_t nrt = cdiv(n_rows, R);
+    const int64_t grid = cdiv(nct, 8) * 8 * nrt;
     if (grid > kMaxBlocks) return fail(DOL_EINVAL, "dol_mix_ring_steps_f32: too large");
     hipLaunchKernelGGL((ring_steps_kernel<S, R>), dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, s, X, ldx, Y, ldy,
-                       n_rows, n4, nct, w_prev, w_next);
+                       n_rows, n4, nct, w_prev, w_next, static_cast<uint32_t>(nrt));
     return check_launch("dol_mix_ring_steps_f32");
   };
   using std::integral_constant;
+  // tile heights measured at 8192 x 2^20 (tools/bench_configs.py ring-eps<S>):
+  // R = 6 for S <= 3, 14 for S = 4, 22 for S = 5-6, 30 for S = 7-8
   switch (steps) {
     case 1: return go(integral_constant<int, 1>{}, integral_constant<int, 4>{});
-    case 2: return go(integral_constant<int, 2>{}, integral_constant<int, 8>{});
-    case 3: return go(integral_constant<int, 3>{}, integral_constant<int, 10>{});
-    case 4: return go(integral_constant<int, 4>{}, integral_constant<int, 12>{});
-    case 5: return go(integral_constant<int, 5>{}, integral_constant<int, 14>{});
-    case 6: return go(integral_constant<int, 6>{}, integral_constant<int, 16>{});
-    case 7: return go(integral_constant<int, 7>{}, integral_constant<int, 16>{});
-    default: return go(integral_constant<int, 8>{}, integral_constant<int, 16>{});
+    case 2: return go(integral_constant<int, 2>{}, integral_constant<int, 6>{});
+    case 3: return go(integral_constant<int, 3>{}, integral_constant<int, 6>{});
+    case 4: return go(integral_constant<int, 4>{}, integral_constant<int, 14>{});
+    case 5: return go(integral_constant<int, 5>{}, integral_constant<int, 22>{});
+    case 6: return go(integral_constant<int, 6>{}, integral_constant<int, 22>{});
+    case 7: return go(integral_constant<int, 7>{}, integral_constant<int, 30>{});
+    default: return go(integral_constant<int, 8>{}, integral_constant<int, 30>{});
   }
 }
 
