@@ -1,0 +1,292 @@
+// dense_split.hip — dense mix Y = W X on the bf16 matrix cores at fp32 accuracy.
+//
+// Dense mixing matrices (communication_graph("compelete", "stochastic", n),
+// Erdos-Renyi and time-varying W; DIST/simulators.py:54-58, :65-70) make the
+// round a GEMM: Y[M,P] = W[M,K] X[K,P], 2 M K P flop.  gfx950 has no
+// reduced-precision f32 MFMA (no xf32) and its exact f32 MFMA runs at 1/16 of
+// the bf16 rate, so this path splits every fp32 operand into three bf16
+// pieces, x = x0 + x1 + x2 exactly (x0 = bf16_rne(x), x1 = bf16_rne(x - x0),
+// x2 = bf16_rne(x - x0 - x1): |x1| <= 2^-8 |x|, |x2| <= 2^-16 |x| and the
+// remainder is 0), and sums the six piece products of scale >= 2^-16 |w x|
+// on v_mfma_f32_32x32x16_bf16:
+//     w x ~= w0 x0 + w0 x1 + w1 x0 + w1 x1 + w0 x2 + w2 x0
+// Each bf16 x bf16 product is exact in fp32 and the MFMA accumulates in fp32,
+// so the result is an fp32-accurate GEMM: the dropped terms (w1 x2, w2 x1,
+// w2 x2) sum to at most 2^-23 |w x|, about one fp32 rounding of the product.  Six bf16 MFMAs
+// cost 6 x 32 = 192 cycles per 32x32x16 block where the f32 MFMA needs
+// 8 x 64 = 512: 2.67x the f32 matrix peak.  Error bound and the tests:
+// tests/test_kernels_gpu.py (test_mix_dense_split3_*).
+//
+// Layout.  A split pass writes both operands in the MFMA's own k-grouping:
+// WA[kg][m][piece][8 bf16] and XB[kg][p][piece][8 bf16] (kg = k / 8, rows
+// m / columns p padded to the 256-tile, k padded to 16, zero filled), so one
+// (row, k-group) record is 48 contiguous bytes holding a lane's three
+// fragments, and a 256-row tile of one k-group is 12 KiB contiguous: the GEMM
+// stages it with 12 LDS-DMA instructions (global_load_lds_dwordx4, no
+// register round trip, no bounds checks) and reads fragments conflict-free
+// (48-B lane stride).
+//
+// GEMM.  256 x 256 output tile per workgroup, 4 waves in 2 x 2, each wave
+// 128 x 128 = 4 x 4 accumulators of 32 x 32 (256 accumulator registers, one
+// wave per SIMD).  K advances 16 per stage (= one MFMA k-step); three stages
+// of 48 KiB in LDS, two in flight while one feeds 96 MFMAs per wave.  Tile
+// order is XCD-aware: workgroup b runs on XCD b % 8, each XCD walks a
+// contiguous range of tiles in groups of 8 row tiles, so the 32 tiles an XCD
+// holds at once share 8 W panels and 4 X panels in its L2.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/dol_hip.h"
+#include "dol_common.h"
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kTile = 256;                            // BM = BN
+constexpr int kRec = 48;                              // bytes per (row, k-group): 3 pieces x 8 bf16
+constexpr int kOpStage = 2 * kTile * kRec;            // 24 KiB: one operand, two k-groups
+constexpr int kStageBytes = 2 * kOpStage;             // 48 KiB
+constexpr int kStages = 3;
+constexpr int kLds = kStages * kStageBytes;           // 144 KiB
+constexpr int kGroupM = 8;                            // row tiles per XCD group
+constexpr int kDmaPerWave = kStageBytes / 1024 / 4;   // 12 LDS-DMA instructions per wave per stage
+
+#define DOL_GPTR(p) ((const __attribute__((address_space(1))) void*)(p))
+#define DOL_LPTR(p) ((__attribute__((address_space(3))) void*)(p))
+
+__device__ __forceinline__ bool finite_bits(uint32_t u) { return (u & 0x7f800000u) != 0x7f800000u; }
+
+// fp32 -> bf16 bits, round to nearest even; NaN stays NaN (quiet), Inf stays Inf
+__device__ __forceinline__ uint32_t bf16_rne(float x) {
+  const uint32_t u = __float_as_uint(x);
+  if (!finite_bits(u)) return (u >> 16) | ((u & 0x7fffffu) ? 0x40u : 0u);
+  return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+}
+
+// x = p0 + p1 + p2 exactly (finite x); non-finite x -> (x, 0, 0)
+__device__ __forceinline__ void split3(float x, uint32_t& p0, uint32_t& p1, uint32_t& p2) {
+  const uint32_t u = __float_as_uint(x);
+  uint32_t h0 = bf16_rne(x);
+  if (finite_bits(u) && (h0 & 0x7f80u) == 0x7f80u) h0 = u >> 16;  // |x| rounds past bf16 max: truncate
+  const float r1 = finite_bits(u) ? x - __uint_as_float(h0 << 16) : 0.f;
+  const uint32_t h1 = bf16_rne(r1);
+  const float r2 = r1 - __uint_as_float(h1 << 16);
+  p0 = h0;
+  p1 = h1;
+  p2 = bf16_rne(r2);
+}
+
+// Split 8 consecutive-k values into one 48-B record (3 x 16 B).
+__device__ __forceinline__ void write_record(const float (&v)[8], uint8_t* dst) {
+  u32x4 q[3];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    uint32_t a0, a1, a2, b0, b1, b2;
+    split3(v[2 * j], a0, a1, a2);
+    split3(v[2 * j + 1], b0, b1, b2);
+    q[0][j] = a0 | (b0 << 16);
+    q[1][j] = a1 | (b1 << 16);
+    q[2][j] = a2 | (b2 << 16);
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) *reinterpret_cast<u32x4*>(dst + 16 * i) = q[i];
+}
+
+// W [M][K] (row stride ldw) -> WA[kg][Mp][48 B]; one thread per (m, kg), m fastest
+__global__ __launch_bounds__(256) void split3_rows_kernel(const float* __restrict__ W, int64_t ldw, int M, int K,
+                                                          int Mp, int Kg, uint8_t* __restrict__ out) {
+  const int64_t idx = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (idx >= int64_t(Mp) * Kg) return;
+  const int m = int(idx % Mp), kg = int(idx / Mp);
+  float v[8];
+  const float* row = W + int64_t(m < M ? m : 0) * ldw;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = 8 * kg + j;
+    v[j] = (m < M && k < K) ? row[k] : 0.f;
+  }
+  write_record(v, out + idx * kRec);
+}
+
+// X [K][P] (row stride ldx) -> XB[kg][Pp][48 B]; one thread per (p, kg), p fastest
+__global__ __launch_bounds__(256) void split3_cols_kernel(const float* __restrict__ X, int64_t ldx, int K, int64_t P,
+                                                          int64_t Pp, int Kg, uint8_t* __restrict__ out) {
+  const int64_t idx = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (idx >= Pp * Kg) return;
+  const int64_t p = idx % Pp;
+  const int kg = int(idx / Pp);
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = 8 * kg + j;
+    v[j] = (p < P && k < K) ? X[int64_t(k) * ldx + p] : 0.f;
+  }
+  write_record(v, out + idx * kRec);
+}
+
+__device__ __forceinline__ void wait_vmcnt_stage(bool more) {
+  if (more) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // kDmaPerWave: the next stage may fly
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+static_assert(kDmaPerWave == 12, "wait_vmcnt_stage assumes 12 DMA instructions per wave per stage");
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void dense_split3_kernel(const uint8_t* __restrict__ WA, const uint8_t* __restrict__ XB, float* __restrict__ Y,
+                         int64_t ldy, int M, int64_t P, int64_t Mp, int64_t Pp, int n_stages, int n_mt,
+                         int64_t n_pt, int64_t tiles_per_xcd) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int64_t j = blockIdx.x >> 3;
+  const int64_t t = (blockIdx.x & 7) * tiles_per_xcd + j;
+  if (j >= tiles_per_xcd || t >= int64_t(n_mt) * n_pt) return;
+  const int64_t per_group = int64_t(kGroupM) * n_pt;
+  const int g = int(t / per_group);
+  const int first_m = g * kGroupM;
+  const int gs = min(n_mt - first_m, kGroupM);
+  const int64_t r = t - int64_t(g) * per_group;
+  const int mt = first_m + int(r % gs);
+  const int64_t pt = r / gs;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int h = lane >> 5, li = lane & 31;
+
+  // stage s holds k-groups 2s, 2s+1 of both operands: [A kg0 | A kg1 | B kg0 | B kg1], 12 KiB each
+  const uint8_t* srcA = WA + int64_t(mt) * kTile * kRec + lane * 16;
+  const uint8_t* srcB = XB + pt * kTile * kRec + lane * 16;
+  const int64_t pitchA = Mp * kRec, pitchB = Pp * kRec;  // bytes per k-group
+  auto issue = [&](int s) {
+    uint8_t* st = lds + (s % kStages) * kStageBytes;
+#pragma unroll
+    for (int i = 0; i < kDmaPerWave; ++i) {
+      const int q = wave + 4 * i;      // 0..47, 1 KiB each
+      const int op = q / 24, qq = q % 24, kgl = qq / 12, chunk = qq % 12;
+      const int64_t kg = 2 * int64_t(s) + kgl;
+      const uint8_t* src = (op == 0 ? srcA + kg * pitchA : srcB + kg * pitchB) + chunk * 1024;
+      __builtin_amdgcn_global_load_lds(DOL_GPTR(src), DOL_LPTR(st + q * 1024), 16, 0, 0);
+    }
+  };
+
+  f32x16 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
+
+  issue(0);
+  if (n_stages > 1) issue(1);
+  for (int s = 0; s < n_stages; ++s) {
+    wait_vmcnt_stage(s + 1 < n_stages);  // my DMA of stage s landed
+    __builtin_amdgcn_s_barrier();        // ... and every wave's; stage (s + 2) % 3 is free
+    if (s + 2 < n_stages) issue(s + 2);
+    const uint8_t* st = lds + (s % kStages) * kStageBytes;
+    const uint8_t* sa = st + h * (kTile * kRec) + (wm * 128 + li) * kRec;
+    const uint8_t* sb = st + kOpStage + h * (kTile * kRec) + (wn * 128 + li) * kRec;
+    bf16x8 fa[4][3], fb[4][3];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        fa[i][p] = *reinterpret_cast<const bf16x8*>(sa + i * 32 * kRec + 16 * p);
+        fb[i][p] = *reinterpret_cast<const bf16x8*>(sb + i * 32 * kRec + 16 * p);
+      }
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        f32x16 c = acc[a][b];
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a][2], fb[b][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a][0], fb[b][2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a][1], fb[b][1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a][1], fb[b][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a][0], fb[b][1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a][0], fb[b][0], c, 0, 0, 0);
+        acc[a][b] = c;
+      }
+  }
+  // C/D map (gfx950): col = lane & 31, row = (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5)
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int64_t col = pt * kTile + wn * 128 + b * 32 + li;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = mt * kTile + wm * 128 + a * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (row < M && col < P) __builtin_nontemporal_store(acc[a][b][e], Y + int64_t(row) * ldy + col);
+      }
+    }
+}
+
+inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+struct Split3Geom {
+  int64_t Mp, Pp, Kg, bytesA, bytesB;
+};
+
+inline Split3Geom geom(int32_t M, int32_t K, int64_t P) {
+  Split3Geom g;
+  g.Mp = cdiv(M, kTile) * kTile;
+  g.Pp = cdiv(P, kTile) * kTile;
+  g.Kg = cdiv(K, 16) * 2;
+  g.bytesA = g.Kg * g.Mp * kRec;
+  g.bytesB = g.Kg * g.Pp * kRec;
+  return g;
+}
+
+}  // namespace
+
+extern "C" int64_t dol_mix_dense_split3_workspace_bytes(int32_t M, int32_t K, int64_t P) {
+  if (M <= 0 || K <= 0 || P <= 0) return 0;
+  const Split3Geom g = geom(M, K, P);
+  return g.bytesA + g.bytesB;
+}
+
+extern "C" int dol_mix_dense_split3_f32(const float* W, int64_t ldw, const float* X, int64_t ldx, float* Y,
+                                        int64_t ldy, int32_t M, int32_t K, int64_t P, void* work,
+                                        int64_t work_bytes, int flags, hipStream_t s) {
+  using dol::fail;
+  if (M < 0 || K < 0 || P < 0) return fail(DOL_EINVAL, "dol_mix_dense_split3_f32: negative size");
+  if (M == 0 || P == 0) return DOL_OK;
+  if (!Y || (K > 0 && (!W || !X))) return fail(DOL_EINVAL, "dol_mix_dense_split3_f32: null pointer");
+  if (ldy < P || (K > 0 && (ldw < K || ldx < P))) return fail(DOL_EINVAL, "dol_mix_dense_split3_f32: ld too small");
+  if (X == Y || W == Y) return fail(DOL_EINVAL, "dol_mix_dense_split3_f32: Y aliases an input");
+  if (K == 0) return hipMemset2DAsync(Y, ldy * 4, 0, P * 4, M, s) == hipSuccess ? DOL_OK
+                     : fail(DOL_EINVAL, "dol_mix_dense_split3_f32: memset failed");
+  const Split3Geom g = geom(M, K, P);
+  if (!work || work_bytes < g.bytesA + g.bytesB)
+    return fail(DOL_EINVAL, "dol_mix_dense_split3_f32: workspace %lld bytes, need %lld",
+                static_cast<long long>(work_bytes), static_cast<long long>(g.bytesA + g.bytesB));
+  if (reinterpret_cast<uintptr_t>(work) % 256) return fail(DOL_EINVAL, "dol_mix_dense_split3_f32: workspace not 256-B aligned");
+  uint8_t* wa = static_cast<uint8_t*>(work);
+  uint8_t* xb = wa + g.bytesA;
+  if (!(flags & DOL_SPLIT3_W_READY)) {
+    const int64_t n = g.Mp * g.Kg;
+    hipLaunchKernelGGL(split3_rows_kernel, dim3(static_cast<unsigned>(cdiv(n, 256))), dim3(256), 0, s, W, ldw, M, K,
+                       static_cast<int>(g.Mp), static_cast<int>(g.Kg), wa);
+  }
+  {
+    const int64_t n = g.Pp * g.Kg;
+    if (cdiv(n, 256) >= (int64_t(1) << 32)) return fail(DOL_EINVAL, "dol_mix_dense_split3_f32: X too large");
+    hipLaunchKernelGGL(split3_cols_kernel, dim3(static_cast<unsigned>(cdiv(n, 256))), dim3(256), 0, s, X, ldx, K, P,
+                       g.Pp, static_cast<int>(g.Kg), xb);
+  }
+  const int n_mt = static_cast<int>(g.Mp / kTile);
+  const int64_t n_pt = g.Pp / kTile;
+  const int64_t tiles_per_xcd = cdiv(int64_t(n_mt) * n_pt, 8);
+  if (8 * tiles_per_xcd >= (int64_t(1) << 32)) return fail(DOL_EINVAL, "dol_mix_dense_split3_f32: too many tiles");
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(dense_split3_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
+    attr = true;
+  }
+  hipLaunchKernelGGL(dense_split3_kernel, dim3(static_cast<unsigned>(8 * tiles_per_xcd)), dim3(256), kLds, s, wa, xb,
+                     Y, ldy, M, P, g.Mp, g.Pp, static_cast<int>(g.Kg / 2), n_mt, n_pt, tiles_per_xcd);
+  return dol::check_launch("dol_mix_dense_split3_f32");
+}

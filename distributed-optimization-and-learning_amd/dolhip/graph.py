@@ -308,9 +308,18 @@ def erdos_renyi_stochastic(n: int, p: float, generator: torch.Generator, device=
 class MixingPlan:
     """Device form of one W: CSR tensors plus the ring specialisation if it applies."""
 
-    def __init__(self, csr: CSR, device, allow_ring: bool = True, dense: bool = False):
+    DENSE_KERNELS = ("split3", "f32")
+
+    def __init__(self, csr: CSR, device, allow_ring: bool = True, dense: bool = False,
+                 dense_kernel: str = "split3"):
         """kind: 'ring' (bit-exact, ring kernel), 'csr' (bit-exact, any W), or
-        'dense' (opt-in: fp32 MFMA GEMM over the dense W, tolerance path)."""
+        'dense' (opt-in tolerance path: a GEMM over the dense W on the matrix
+        cores; dense_kernel 'split3' = three-piece bf16 split at fp32 accuracy,
+        'f32' = exact-f32 MFMA fma chain)."""
+        if dense_kernel not in self.DENSE_KERNELS:
+            raise ValueError(f"dense_kernel must be one of {self.DENSE_KERNELS}")
+        self.dense_kernel = dense_kernel
+        self._work, self._work_key = None, None
         self.csr = csr
         self.device = torch.device(device)
         self.n_rows = csr.n_rows
@@ -333,12 +342,16 @@ class MixingPlan:
         return self.csr.nnz / max(1, self.csr.n_rows * self.csr.n_cols)
 
     @classmethod
-    def from_dense(cls, W: torch.Tensor) -> "MixingPlan":
+    def from_dense(cls, W: torch.Tensor, dense_kernel: str = "split3") -> "MixingPlan":
         """A 'dense' plan straight from a device W (no CSR; e.g. a per-round
-        erdos_renyi_stochastic draw).  Only apply() (fp32 MFMA) is available."""
+        erdos_renyi_stochastic draw).  Only apply() (matrix cores) is available."""
         if W.device.type != "cuda" or W.dtype != torch.float32 or W.dim() != 2:
             raise ValueError("from_dense: expected a 2-D float32 CUDA tensor")
+        if dense_kernel not in cls.DENSE_KERNELS:
+            raise ValueError(f"dense_kernel must be one of {cls.DENSE_KERNELS}")
         plan = cls.__new__(cls)
+        plan.dense_kernel = dense_kernel
+        plan._work, plan._work_key = None, None
         plan.csr = None
         plan.device = W.device
         plan.n_rows = W.shape[0]
@@ -347,8 +360,24 @@ class MixingPlan:
         return plan
 
     @classmethod
-    def from_graph(cls, W: Graph, device, allow_ring: bool = True, dense: bool = False) -> "MixingPlan":
-        return cls(csr_from_dense(W), device, allow_ring, dense)
+    def from_graph(cls, W: Graph, device, allow_ring: bool = True, dense: bool = False,
+                   dense_kernel: str = "split3") -> "MixingPlan":
+        return cls(csr_from_dense(W), device, allow_ring, dense, dense_kernel)
+
+    def _mix_dense(self, X: torch.Tensor, Y: torch.Tensor, P: Optional[int]) -> torch.Tensor:
+        from . import ops
+        if self.dense_kernel == "f32":
+            return ops.mix_dense(self.W, X, Y, P=P)
+        P = X.shape[1] if P is None else P
+        M, K = self.W.shape
+        key = (M, K, int(P), X.device)
+        ready = self._work_key == key  # this plan's W already split into the workspace
+        if not ready:
+            self._work = torch.empty(max(ops.dense_split3_workspace_bytes(M, K, P), 1), dtype=torch.uint8,
+                                     device=X.device)
+        ops.mix_dense_split3(self.W, X, Y, P=P, work=self._work, w_ready=ready)
+        self._work_key = key
+        return Y
 
     MAX_FUSED_STEPS = 8
 
@@ -371,7 +400,7 @@ class MixingPlan:
         if self.kind == "ring":
             return ops.mix_ring(X, Y, self.w_prev, self.w_next, P=P, n_rows=self.n_rows)
         if self.kind == "dense":
-            return ops.mix_dense(self.W, X, Y, P=P)
+            return self._mix_dense(X, Y, P)
         return ops.mix_csr(X, Y, self.rowptr, self.col, self.val, P=P)
 
 

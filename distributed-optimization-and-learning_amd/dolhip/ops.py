@@ -14,7 +14,8 @@ from . import _native
 from ._native import DolNativeError
 
 __all__ = [
-    "DolNativeError", "mix_csr", "mix_ring", "mix_dense", "mix_ring_steps", "prox_admm_sgd", "admm_dual", "ordered_mean",
+    "DolNativeError", "mix_csr", "mix_ring", "mix_dense", "mix_dense_split3", "dense_split3_workspace_bytes",
+    "mix_ring_steps", "prox_admm_sgd", "admm_dual", "ordered_mean",
     "ordered_sum", "stream_copy", "dual_workspace_bytes", "prox_grad", "admm_step_dual", "mlp_step",
     "dgd_ring", "dgd_csr", "OBJECTIVES",
 ]
@@ -186,6 +187,38 @@ def mix_dense(W: torch.Tensor, X: torch.Tensor, Y: torch.Tensor, P: Optional[int
     if X.data_ptr() == Y.data_ptr():
         raise ValueError("X and Y alias")
     _native.call("dol_mix_dense_f32", W.data_ptr(), ldw, X.data_ptr(), ldx, Y.data_ptr(), ldy, M, K, P, _stream(X))
+    return Y
+
+
+def dense_split3_workspace_bytes(M: int, K: int, P: int) -> int:
+    return int(_native.lib().dol_mix_dense_split3_workspace_bytes(int(M), int(K), int(P)))
+
+
+def mix_dense_split3(W: torch.Tensor, X: torch.Tensor, Y: torch.Tensor, P: Optional[int] = None,
+                     work: Optional[torch.Tensor] = None, w_ready: bool = False) -> torch.Tensor:
+    """Y = W X on the bf16 matrix cores at fp32 accuracy (dol_mix_dense_split3_f32:
+    three-piece bf16 split of both operands, six piece products per term).
+    `work`: a uint8 device buffer of >= dense_split3_workspace_bytes(M, K, P)
+    bytes (allocated per call when None); w_ready=True reuses the split W that
+    a previous call with the same W left in `work`."""
+    P = X.shape[1] if P is None else P
+    ldw = _check_rows("W", W)
+    ldx = _check_rows("X", X, P)
+    ldy = _check_rows("Y", Y, P)
+    M, K = W.shape
+    if X.shape[0] < K or Y.shape[0] < M:
+        raise ValueError(f"shapes: W {tuple(W.shape)}, X {tuple(X.shape)}, Y {tuple(Y.shape)}")
+    if Y.data_ptr() in (X.data_ptr(), W.data_ptr()):
+        raise ValueError("Y aliases an input")
+    need = dense_split3_workspace_bytes(M, K, P)
+    if work is None:
+        if w_ready:
+            raise ValueError("w_ready needs the workspace of the call that split W")
+        work = torch.empty(max(need, 1), dtype=torch.uint8, device=X.device)
+    elif work.device != X.device or work.dtype != torch.uint8 or work.numel() < need:
+        raise ValueError(f"work: need a uint8 tensor of >= {need} bytes on {X.device}")
+    _native.call("dol_mix_dense_split3_f32", W.data_ptr(), ldw, X.data_ptr(), ldx, Y.data_ptr(), ldy, M, K, P,
+                 work.data_ptr(), work.numel(), 1 if w_ready else 0, _stream(X))
     return Y
 
 

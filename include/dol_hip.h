@@ -104,6 +104,25 @@ int dol_mix_dense_f32(const float* W, int64_t ldw, const float* X, int64_t ldx,
                       hipStream_t s);
 
 /*
+ * Dense mix on the bf16 matrix cores at fp32 accuracy ("split3"): the same
+ * Y[M,P] = W[M,K] . X[K,P] and the same reference call sites as
+ * dol_mix_dense_f32 (DIST/simulators.py:54-70 + DIST/clients.py:61-69), with
+ * every operand split into three bf16 pieces (exact) and the six leading
+ * piece products summed on v_mfma_f32_32x32x16_bf16 in fp32: 2.67x the
+ * exact-f32 MFMA rate.  Error: |Y - W.X| <= (gamma_{6K'} + 2^-23) sum|W||X|
+ * with gamma in units of 2^-23 (K' = K rounded up to 16); tests state the
+ * observed maximum.  Subnormal pieces (|value| < ~1e-33) may be flushed.
+ * `work` (>= dol_mix_dense_split3_workspace_bytes(M, K, P), 256-B aligned)
+ * receives the split operands; flags & DOL_SPLIT3_W_READY reuses the split W
+ * a previous call left in `work` (same W, M, K, P).  Y must not alias W or X.
+ */
+#define DOL_SPLIT3_W_READY 1
+int dol_mix_dense_split3_f32(const float* W, int64_t ldw, const float* X, int64_t ldx,
+                             float* Y, int64_t ldy, int32_t M, int32_t K, int64_t P,
+                             void* work, int64_t work_bytes, int flags, hipStream_t s);
+int64_t dol_mix_dense_split3_workspace_bytes(int32_t M, int32_t K, int64_t P);
+
+/*
  * One round of decentralised gradient descent on a separable synthetic loss
  * (BASELINE config 3), fused: the gossip mix of dol_mix_ring_f32 /
  * dol_mix_csr_f32 (same arguments, same bit-exact mix), then `local_steps`

@@ -311,7 +311,7 @@ def test_mix_dense_identity_and_permutation_exact(M, K, P, gpu):
 def test_mix_dense_stochastic_within_gamma_bound(n, P, gpu):
     torch.manual_seed(2028)
     Wt = G.communication_graph("compelete", "stochastic", n)[0]
-    plan = G.MixingPlan.from_graph(Wt, gpu, dense=True)
+    plan = G.MixingPlan.from_graph(Wt, gpu, dense=True, dense_kernel="f32")
     assert plan.kind == "dense"
     rng = np.random.default_rng(n)
     X = rng.standard_normal((n, P)).astype(np.float32)
@@ -325,6 +325,93 @@ def test_mix_dense_stochastic_within_gamma_bound(n, P, gpu):
     # and close to the bit-exact CSR path
     exact = oracle.mix_csr(X, plan.csr.rowptr, plan.csr.col, plan.csr.val)
     assert np.all(np.abs(Y.cpu().numpy() - exact) <= 2 * _gamma_bound(Wd, X) + 1e-30)
+
+
+def _split3_bound(W, X):
+    """Bound for the split3 path (dol_hip.h): the dropped piece products
+    (<= 2^-23 |w x| each term) plus fp32 accumulation of 6 K' piece products,
+    priced at u = 2^-23 so it holds for any rounding mode inside the MFMA."""
+    K = -(-W.shape[1] // 16) * 16
+    u = 2.0 ** -23
+    n = 6 * K
+    return (n * u / (1 - n * u) + 2.0 ** -23) * (np.abs(W.astype(np.float64)) @ np.abs(X.astype(np.float64)))
+
+
+@pytest.mark.parametrize("M,K,P", [(256, 256, 1024), (130, 37, 1031), (64, 64, 3), (513, 300, 700)])
+def test_mix_dense_split3_identity_and_permutation_exact(M, K, P, gpu):
+    """One weight of 1.0 per row: the three pieces of x re-sum exactly."""
+    rng = np.random.default_rng(M + K + 1)
+    X = rng.standard_normal((K, P)).astype(np.float32)
+    X[0, :3] = [3.0e38, -1.0e-30, 0.0]  # near the top of the range (truncated x0), tiny, zero
+    for name in ("id", "perm"):
+        W = np.zeros((M, K), np.float32)
+        src = np.arange(M) % K if name == "id" else rng.integers(0, K, M)
+        W[np.arange(M), src] = 1.0
+        Y = torch.empty(M, P, device=gpu)
+        ops.mix_dense_split3(dev(W, gpu), dev(X, gpu), Y)
+        torch.cuda.synchronize()
+        assert bits_equal(Y.cpu().numpy(), X[src]), name
+
+
+@pytest.mark.parametrize("n,P,extra", [(16, 4099, 0), (256, 8192, 3), (1000, 513, 0), (300, 20000, 5)])
+def test_mix_dense_split3_stochastic_within_bound(n, P, extra, gpu):
+    """complete/stochastic W (DIST/simulators.py:54-58,65-70) through the plan:
+    within the rigorous bound vs fp64, and at least as close to fp64 as the
+    reference's own sequential fp32 sum (oracle.mix_csr) up to 2x."""
+    torch.manual_seed(2028)
+    Wt = G.communication_graph("compelete", "stochastic", n)[0]
+    plan = G.MixingPlan.from_graph(Wt, gpu, dense=True, dense_kernel="split3")
+    rng = np.random.default_rng(n + 7)
+    X = rng.standard_normal((n, P)).astype(np.float32)
+    Xd = padded(X, gpu, extra)
+    Y = padded(np.zeros_like(X), gpu, extra)
+    for it in range(2):  # second call reuses the split W (w_ready)
+        Y.fill_(float("nan"))
+        plan.apply(Xd, Y, P=P)
+        torch.cuda.synchronize()
+        got = Y[:, :P].cpu().numpy()
+        assert np.isnan(Y[:, P:].cpu().numpy()).all()  # padding untouched
+        Wd = plan.csr.dense()
+        want64 = Wd.astype(np.float64) @ X.astype(np.float64)
+        err = np.abs(got.astype(np.float64) - want64)
+        assert np.all(err <= _split3_bound(Wd, X) + 1e-30), it
+        ref = oracle.mix_csr(X, plan.csr.rowptr, plan.csr.col, plan.csr.val)
+        ref_err = np.abs(ref.astype(np.float64) - want64)
+        assert err.max() <= 2 * ref_err.max() + 1e-30, (err.max(), ref_err.max())
+        assert np.sqrt((err ** 2).mean()) <= 2 * np.sqrt((ref_err ** 2).mean()) + 1e-30
+
+
+def test_mix_dense_split3_matches_f32_kernel_and_ragged_rows(gpu):
+    """Erdos-Renyi-style W with M != K (a row block) against the exact-f32 MFMA
+    kernel and fp64; the W_READY reuse must give the same bits as a fresh split."""
+    rng = np.random.default_rng(5)
+    M, K, P = 200, 777, 3001
+    A = (rng.random((M, K)) < 0.1).astype(np.float32)
+    W = (A * rng.random((M, K))).astype(np.float32)
+    X = (rng.standard_normal((K, P)) * 10.0 ** rng.integers(-3, 4, (K, 1))).astype(np.float32)
+    Wd, Xd = dev(W, gpu), dev(X, gpu)
+    Y1, Y2, Y3 = (torch.empty(M, P, device=gpu) for _ in range(3))
+    work = torch.empty(ops.dense_split3_workspace_bytes(M, K, P), dtype=torch.uint8, device=gpu)
+    ops.mix_dense_split3(Wd, Xd, Y1, work=work)
+    ops.mix_dense_split3(Wd, Xd, Y2, work=work, w_ready=True)
+    ops.mix_dense(Wd, Xd, Y3)
+    torch.cuda.synchronize()
+    assert bits_equal(Y1.cpu().numpy(), Y2.cpu().numpy())
+    want64 = W.astype(np.float64) @ X.astype(np.float64)
+    e_split = np.abs(Y1.cpu().numpy() - want64)
+    e_f32 = np.abs(Y3.cpu().numpy() - want64)
+    assert np.all(e_split <= _split3_bound(W, X) + 1e-30)
+    assert e_split.max() <= 2 * e_f32.max() + 1e-30
+
+
+def test_mix_dense_split3_argument_errors(gpu):
+    W = torch.zeros(8, 8, device=gpu)
+    X = torch.zeros(8, 16, device=gpu)
+    with pytest.raises(ValueError):
+        ops.mix_dense_split3(W, X, X)
+    small = torch.empty(16, dtype=torch.uint8, device=gpu)
+    with pytest.raises(ValueError):
+        ops.mix_dense_split3(W, X, torch.empty(8, 16, device=gpu), work=small)
 
 
 @pytest.mark.parametrize("admm", [False, True])
