@@ -35,6 +35,7 @@
 // holds at once share 8 W panels and 4 X panels in its L2.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/dol_hip.h"
 #include "dol_common.h"
@@ -133,18 +134,26 @@ __device__ __forceinline__ void wait_vmcnt_stage(bool more) {
 }
 static_assert(kDmaPerWave == 12, "wait_vmcnt_stage assumes 12 DMA instructions per wave per stage");
 
+// PROBE (tools only, DOL_SPLIT3_PROBE): 1 = no operand staging (MFMA ceiling of
+// the loop), 2 = staging only (no fragment reads / MFMAs).  Measured at 8192 x
+// 101770 (profiles/r01c_dense_split3_probe.txt): full 53 ms, MFMA-only 45 ms,
+// staging-only 20 ms.  Tried and dropped (same box, no gain): fragments
+// double-buffered in registers with the DMA three stages ahead; the
+// v_mfma_f32_16x16x32_bf16 shape with (k-group, piece pair) k slots (same
+// speed, and mixing piece scales inside one MFMA loses exactness of x0+x1+x2).
+template <int PROBE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void dense_split3_kernel(const uint8_t* __restrict__ WA, const uint8_t* __restrict__ XB, float* __restrict__ Y,
                          int64_t ldy, int M, int64_t P, int64_t Mp, int64_t Pp, int n_stages, int n_mt,
-                         int64_t n_pt, int64_t tiles_per_xcd) {
+                         int64_t n_pt, int64_t tiles_per_xcd, int group_m) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int64_t j = blockIdx.x >> 3;
   const int64_t t = (blockIdx.x & 7) * tiles_per_xcd + j;
   if (j >= tiles_per_xcd || t >= int64_t(n_mt) * n_pt) return;
-  const int64_t per_group = int64_t(kGroupM) * n_pt;
+  const int64_t per_group = int64_t(group_m) * n_pt;
   const int g = int(t / per_group);
-  const int first_m = g * kGroupM;
-  const int gs = min(n_mt - first_m, kGroupM);
+  const int first_m = g * group_m;
+  const int gs = min(n_mt - first_m, group_m);
   const int64_t r = t - int64_t(g) * per_group;
   const int mt = first_m + int(r % gs);
   const int64_t pt = r / gs;
@@ -159,6 +168,7 @@ void dense_split3_kernel(const uint8_t* __restrict__ WA, const uint8_t* __restri
   const uint8_t* srcB = XB + pt * kTile * kRec + lane * 16;
   const int64_t pitchA = Mp * kRec, pitchB = Pp * kRec;  // bytes per k-group
   auto issue = [&](int s) {
+    if constexpr (PROBE == 1) return;
     uint8_t* st = lds + (s % kStages) * kStageBytes;
 #pragma unroll
     for (int i = 0; i < kDmaPerWave; ++i) {
@@ -178,16 +188,10 @@ void dense_split3_kernel(const uint8_t* __restrict__ WA, const uint8_t* __restri
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
 
-  issue(0);
-  if (n_stages > 1) issue(1);
-  for (int s = 0; s < n_stages; ++s) {
-    wait_vmcnt_stage(s + 1 < n_stages);  // my DMA of stage s landed
-    __builtin_amdgcn_s_barrier();        // ... and every wave's; stage (s + 2) % 3 is free
-    if (s + 2 < n_stages) issue(s + 2);
+  auto read_frags = [&](int s, bf16x8 (&fa)[4][3], bf16x8 (&fb)[4][3]) {
     const uint8_t* st = lds + (s % kStages) * kStageBytes;
     const uint8_t* sa = st + h * (kTile * kRec) + (wm * 128 + li) * kRec;
     const uint8_t* sb = st + kOpStage + h * (kTile * kRec) + (wn * 128 + li) * kRec;
-    bf16x8 fa[4][3], fb[4][3];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -195,6 +199,10 @@ void dense_split3_kernel(const uint8_t* __restrict__ WA, const uint8_t* __restri
         fa[i][p] = *reinterpret_cast<const bf16x8*>(sa + i * 32 * kRec + 16 * p);
         fb[i][p] = *reinterpret_cast<const bf16x8*>(sb + i * 32 * kRec + 16 * p);
       }
+  };
+  // the six piece products of one 32x32x16 block, smallest first
+  auto mfmas = [&](const bf16x8 (&fa)[4][3], const bf16x8 (&fb)[4][3]) {
+    __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
@@ -208,6 +216,23 @@ void dense_split3_kernel(const uint8_t* __restrict__ WA, const uint8_t* __restri
         c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a][0], fb[b][0], c, 0, 0, 0);
         acc[a][b] = c;
       }
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto barrier = [] {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");  // keep LDS reads below the barrier
+  };
+
+  issue(0);
+  if (n_stages > 1) issue(1);
+  for (int s = 0; s < n_stages; ++s) {
+    wait_vmcnt_stage(s + 1 < n_stages);  // my DMA of stage s landed
+    barrier();                           // ... and every wave's; stage (s + 2) % 3 is free
+    if (s + 2 < n_stages) issue(s + 2);
+    if constexpr (PROBE == 2) continue;
+    bf16x8 fa[4][3], fb[4][3];
+    read_frags(s, fa, fb);
+    mfmas(fa, fb);
   }
   // C/D map (gfx950): col = lane & 31, row = (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5)
 #pragma unroll
@@ -280,13 +305,23 @@ extern "C" int dol_mix_dense_split3_f32(const float* W, int64_t ldw, const float
   const int64_t n_pt = g.Pp / kTile;
   const int64_t tiles_per_xcd = cdiv(int64_t(n_mt) * n_pt, 8);
   if (8 * tiles_per_xcd >= (int64_t(1) << 32)) return fail(DOL_EINVAL, "dol_mix_dense_split3_f32: too many tiles");
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(dense_split3_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
-    attr = true;
+  static int probe = -1, group_m = kGroupM;
+  if (probe < 0) {
+    const char* e = getenv("DOL_SPLIT3_PROBE");
+    probe = e ? atoi(e) : 0;
+    const char* gm = getenv("DOL_SPLIT3_GROUP_M");
+    if (gm && atoi(gm) > 0) group_m = atoi(gm);
+    for (const void* k : {reinterpret_cast<const void*>(dense_split3_kernel<0>),
+                          reinterpret_cast<const void*>(dense_split3_kernel<1>),
+                          reinterpret_cast<const void*>(dense_split3_kernel<2>)})
+      (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
   }
-  hipLaunchKernelGGL(dense_split3_kernel, dim3(static_cast<unsigned>(8 * tiles_per_xcd)), dim3(256), kLds, s, wa, xb,
-                     Y, ldy, M, P, g.Mp, g.Pp, static_cast<int>(g.Kg / 2), n_mt, n_pt, tiles_per_xcd);
+  auto launch = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(8 * tiles_per_xcd)), dim3(256), kLds, s, wa, xb, Y, ldy, M,
+                       P, g.Mp, g.Pp, static_cast<int>(g.Kg / 2), n_mt, n_pt, tiles_per_xcd, group_m);
+  };
+  if (probe == 1) launch(dense_split3_kernel<1>);
+  else if (probe == 2) launch(dense_split3_kernel<2>);
+  else launch(dense_split3_kernel<0>);
   return dol::check_launch("dol_mix_dense_split3_f32");
 }
