@@ -392,7 +392,10 @@ __global__ __launch_bounds__(kThreads) void csr_mix_kernel(
 // re-reads of each row hit there.  Placement is a speed assumption only: any
 // other block->XCD mapping gives the same results.  Measured at 8192 x 2^20,
 // d = 4 (tools/membench6.hip): 4.04 TB/s vs 3.0 with 4 KiB tiles whose 32 MiB
-// slabs re-read through the Infinity Cache.
+// slabs re-read through the Infinity Cache.  Degree-4 rows (random-regular)
+// gather all passes' indices before any neighbour load (16.68 vs 16.80 ms).
+// A persistent variant (a fixed grid per XCD walking the tiles in step, so
+// only one slab is live in L2) ran 25-46 ms: latency-bound, dropped.
 template <int W, int PASSES, class Epi = NoEpi>
 __global__ __launch_bounds__(kThreads) void csr_xcd_kernel(
     const float* __restrict__ X, int64_t ldx, float* __restrict__ Y, int64_t ldy, int n_rows,
@@ -409,15 +412,55 @@ __global__ __launch_bounds__(kThreads) void csr_xcd_kernel(
   const int64_t c = int64_t(ct) * W + lane_c;  // f4 column
   const f4* xb = reinterpret_cast<const f4*>(X) + c;
   const int64_t ldv = ldx / 4;
+  // every pass's row extent first, then (degree-4 rows, the random-regular
+  // case) every pass's neighbour indices, then all neighbour loads: three
+  // dependent round trips per workgroup instead of three per pass
+  int rr[PASSES], e0[PASSES], e1[PASSES];
+  bool four = true;
 #pragma unroll
   for (int p = 0; p < PASSES; ++p) {
-    const int r = int(rb) * RB + p * ROWS + lane_r;
+    rr[p] = int(rb) * RB + p * ROWS + lane_r;
+    const int rc = rr[p] < n_rows ? rr[p] : n_rows - 1;
+    e0[p] = rowptr[rc];
+    e1[p] = rowptr[rc + 1];
+    four = four && (e1[p] - e0[p] == 4);
+  }
+  if (four) {
+    int cc[PASSES][4];
+    float vv[PASSES][4];
+#pragma unroll
+    for (int p = 0; p < PASSES; ++p)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        cc[p][q] = col[e0[p] + q];
+        vv[p][q] = val[e0[p] + q];
+      }
+    f4 xs[PASSES][4];
+#pragma unroll
+    for (int p = 0; p < PASSES; ++p)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) xs[p][q] = xb[int64_t(cc[p][q]) * ldv];
+#pragma unroll
+    for (int p = 0; p < PASSES; ++p) {
+      if (rr[p] < n_rows) {
+        const auto es = epi.template load<f4>(rr[p], 4 * c);
+        f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc = fmac(acc, vv[p][q], xs[p][q]);
+        acc = epi.apply(acc, es, rr[p], 4 * c);
+        __builtin_nontemporal_store(acc, reinterpret_cast<f4*>(Y + int64_t(rr[p]) * ldy) + c);
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int p = 0; p < PASSES; ++p) {
+    const int r = rr[p];
     if (r < n_rows) {
       const auto es = epi.template load<f4>(r, 4 * c);
       f4 acc = f4{0.f, 0.f, 0.f, 0.f};
-      const int e1 = rowptr[r + 1];
-      int e = rowptr[r];
-      for (; e + 4 <= e1; e += 4) {
+      int e = e0[p];
+      for (; e + 4 <= e1[p]; e += 4) {
         const f4 x0 = xb[int64_t(col[e]) * ldv], x1 = xb[int64_t(col[e + 1]) * ldv];
         const f4 x2 = xb[int64_t(col[e + 2]) * ldv], x3 = xb[int64_t(col[e + 3]) * ldv];
         acc = fmac(acc, val[e], x0);
@@ -425,7 +468,7 @@ __global__ __launch_bounds__(kThreads) void csr_xcd_kernel(
         acc = fmac(acc, val[e + 2], x2);
         acc = fmac(acc, val[e + 3], x3);
       }
-      for (; e < e1; ++e) acc = fmac(acc, val[e], xb[int64_t(col[e]) * ldv]);
+      for (; e < e1[p]; ++e) acc = fmac(acc, val[e], xb[int64_t(col[e]) * ldv]);
       acc = epi.apply(acc, es, r, 4 * c);
       __builtin_nontemporal_store(acc, reinterpret_cast<f4*>(Y + int64_t(r) * ldy) + c);
     }
@@ -886,12 +929,20 @@ int mix_csr_impl(const char* nm, const float* X, int64_t ldx, int32_t x_rows, fl
   int64_t done4 = 0;
   if (use_xcd) {
     const int64_t ntiles = cs.n4 / XW;
-    const int64_t nrb = cdiv(n_rows, (kThreads / XW) * XPASSES);
-    const int64_t grid = cdiv(ntiles, 8) * 8 * nrb;
-    if (grid > kMaxBlocks * 8) return fail(DOL_EINVAL, "%s: problem too large for one launch", nm);
-    hipLaunchKernelGGL((csr_xcd_kernel<XW, XPASSES, Epi>), dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, s, X,
-                       ldx, Y, ldy, n_rows, static_cast<uint32_t>(nrb), static_cast<uint32_t>(ntiles), rowptr, col, val,
-                       epi);
+    const int passes = env_int("DOL_CSR_PASSES", XPASSES);
+    auto go = [&](auto pc) {
+      constexpr int PS = decltype(pc)::value;
+      const int64_t nrb = cdiv(n_rows, (kThreads / XW) * PS);
+      const int64_t grid = cdiv(ntiles, 8) * 8 * nrb;
+      if (grid > kMaxBlocks * 8) return false;
+      hipLaunchKernelGGL((csr_xcd_kernel<XW, PS, Epi>), dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, s, X,
+                         ldx, Y, ldy, n_rows, static_cast<uint32_t>(nrb), static_cast<uint32_t>(ntiles), rowptr, col,
+                         val, epi);
+      return true;
+    };
+    const bool ok = passes == 1 ? go(std::integral_constant<int, 1>{})
+                    : passes == 4 ? go(std::integral_constant<int, 4>{}) : go(std::integral_constant<int, XPASSES>{});
+    if (!ok) return fail(DOL_EINVAL, "%s: problem too large for one launch", nm);
     done4 = ntiles * XW;
   }
   if (cs.n4 > done4)  // column offset through c_off so the epilogue sees absolute columns
