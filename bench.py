@@ -51,7 +51,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline (profiling runs)")
     ap.add_argument("--no-copy", action="store_true", help="skip the copy-kernel calibration")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_ring_8192x1M.json"))
-    ap.add_argument("--no-primal-dual", action="store_true", help="skip the secondary primal/dual round")
+    ap.add_argument("--no-primal-dual", action="store_true", help="skip the secondary measurements (primal/dual round, FedLCon eps=5, dense ER mix)")
     ap.add_argument("--pd-steps", type=int, default=10)
     return ap.parse_args()
 
@@ -187,6 +187,36 @@ def primal_dual_round(N: int, P: int, world: int, rank: int, device, steps: int)
             "kernels": kern}
 
 
+def dense_mix_round(device, N: int = 1024, P: int = 101770, reps: int = 10):
+    """Secondary (BASELINE config 5's mixing, N = 1): X <- W X with an Erdos-Renyi
+    p = 0.1 stochastic W (graph.erdos_renyi_stochastic, drawn on the device) on
+    the split3 bf16-MFMA kernel (dense_split.hip), P = the 784-128-10 MLP's
+    parameter count.  Includes the per-round operand split; flop = 2 N^2 P."""
+    from dolhip import graph as G, ops
+    from dolhip.bank import row_stride
+    gen = torch.Generator(device=device).manual_seed(2028)
+    W = G.erdos_renyi_stochastic(N, 0.1, gen)
+    X = torch.empty(N, row_stride(P), device=device).normal_(generator=gen)
+    Y = torch.empty_like(X)
+    work = torch.empty(ops.dense_split3_workspace_bytes(N, N, P), dtype=torch.uint8, device=device)
+    ops.mix_dense_split3(W, X, Y, P=P, work=work)
+    torch.cuda.synchronize(device)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        ops.mix_dense_split3(W, X, Y, P=P, work=work)
+    e.record()
+    torch.cuda.synchronize(device)
+    ms = s.elapsed_time(e) / reps
+    tf = 2.0 * N * N * P / (ms / 1e3) / 1e12
+    del W, X, Y, work
+    torch.cuda.empty_cache()
+    return {"agents": N, "params": P, "ms_per_round": ms, "rounds_per_s": 1e3 / ms, "TFLOPs_f32_equiv": tf,
+            "vs_f32_matrix_peak_157TF": tf / 157.3, "bf16_mfma_util": 6 * tf / 2516.6,
+            "what": "dense ER p=0.1 W mix on bf16 MFMA at fp32 accuracy (three-piece split, six products), "
+                    "split pass included"}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -279,6 +309,9 @@ def main():
     pd_round = None
     if not args.no_primal_dual:
         pd_round = primal_dual_round(N, P, world, rank, device, args.pd_steps)
+    dense = None
+    if world == 1 and not args.no_primal_dual:
+        dense = dense_mix_round(device)
 
     traffic = None
     traffic_src = None
@@ -336,6 +369,7 @@ def main():
             "cpu_baseline": cpu,
             "primal_dual_round": pd_round,
             "fedlcon_eps5": fedlcon,
+            "dense_er_mix": dense,
         }
         print(json.dumps(out), flush=True)
     if world > 1:
