@@ -198,7 +198,7 @@ def dense_mix_round(device, N: int = 1024, P: int = 101770, reps: int = 10):
     W = G.erdos_renyi_stochastic(N, 0.1, gen)
     X = torch.empty(N, row_stride(P), device=device).normal_(generator=gen)
     Y = torch.empty_like(X)
-    work = torch.empty(ops.dense_split3_workspace_bytes(N, N, P), dtype=torch.uint8, device=device)
+    work = torch.empty(ops.dense_split3_workspace_bytes(N, N, P, 0), dtype=torch.uint8, device=device)
     ops.mix_dense_split3(W, X, Y, P=P, work=work)
     torch.cuda.synchronize(device)
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -54,6 +54,11 @@ constexpr int kStages = 3;
 constexpr int kLds = kStages * kStageBytes;           // 144 KiB
 constexpr int kGroupM = 8;                            // row tiles per XCD group
 constexpr int kDmaPerWave = kStageBytes / 1024 / 4;   // 12 LDS-DMA instructions per wave per stage
+// fused-X variant: B staged as fp32 rows (16 k x 256 p, 1040-B pitch so the two
+// lane halves' rows 8 apart fall on different banks) and split in registers
+constexpr int kBPitch = 1040;
+constexpr int kStageFX = kOpStage + 16 * kBPitch;     // 41216 B
+constexpr int kDmaFX = (24 + 16) / 4;                  // 10 per wave per stage
 
 #define DOL_GPTR(p) ((const __attribute__((address_space(1))) void*)(p))
 #define DOL_LPTR(p) ((__attribute__((address_space(3))) void*)(p))
@@ -128,11 +133,60 @@ __global__ __launch_bounds__(256) void split3_cols_kernel(const float* __restric
   write_record(v, out + idx * kRec);
 }
 
+template <bool FX>
 __device__ __forceinline__ void wait_vmcnt_stage(bool more) {
-  if (more) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // kDmaPerWave: the next stage may fly
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (!more) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if (FX) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // kDmaFX: the next stage may fly
+  else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");          // kDmaPerWave
 }
-static_assert(kDmaPerWave == 12, "wait_vmcnt_stage assumes 12 DMA instructions per wave per stage");
+static_assert(kDmaPerWave == 12 && kDmaFX == 10, "wait_vmcnt_stage assumes 12 / 10 DMA instructions per wave");
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
+
+// split3() of 8 values into three bf16x8 fragments with v_cvt_pk_bf16_f32 (RNE,
+// the same rounding as bf16_rne), bit-identical to the split pass; a wave with
+// any non-finite or |x| >= 0x7f7f8000 value takes split3() itself
+__device__ __forceinline__ void split8(const float (&v)[8], bf16x8& p0, bf16x8& p1, bf16x8& p2) {
+  bool bad = false;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bad |= !(__builtin_fabsf(v[j]) < __uint_as_float(0x7f7f8000u));
+  if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
+    u32x4 q[3];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      uint32_t a0, a1, a2, b0, b1, b2;
+      split3(v[2 * j], a0, a1, a2);
+      split3(v[2 * j + 1], b0, b1, b2);
+      q[0][j] = a0 | (b0 << 16);
+      q[1][j] = a1 | (b1 << 16);
+      q[2][j] = a2 | (b2 << 16);
+    }
+    p0 = __builtin_bit_cast(bf16x8, q[0]);
+    p1 = __builtin_bit_cast(bf16x8, q[1]);
+    p2 = __builtin_bit_cast(bf16x8, q[2]);
+    return;
+  }
+  bf2 a[4], b[4], c[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const f2 x = {v[2 * j], v[2 * j + 1]};
+    a[j] = __builtin_convertvector(x, bf2);
+    const f2 r1 = x - __builtin_convertvector(a[j], f2);
+    b[j] = __builtin_convertvector(r1, bf2);
+    const f2 r2 = r1 - __builtin_convertvector(b[j], f2);
+    c[j] = __builtin_convertvector(r2, bf2);
+  }
+  auto cat = [](const bf2 (&w)[4]) {
+    const bf4 lo = __builtin_shufflevector(w[0], w[1], 0, 1, 2, 3);
+    const bf4 hi = __builtin_shufflevector(w[2], w[3], 0, 1, 2, 3);
+    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  };
+  p0 = cat(a);
+  p1 = cat(b);
+  p2 = cat(c);
+}
 
 // PROBE (tools only, DOL_SPLIT3_PROBE): 1 = no operand staging (MFMA ceiling of
 // the loop), 2 = staging only (no fragment reads / MFMAs).  Measured at 8192 x
@@ -141,11 +195,16 @@ static_assert(kDmaPerWave == 12, "wait_vmcnt_stage assumes 12 DMA instructions p
 // double-buffered in registers with the DMA three stages ahead; the
 // v_mfma_f32_16x16x32_bf16 shape with (k-group, piece pair) k slots (same
 // speed, and mixing piece scales inside one MFMA loses exactness of x0+x1+x2).
-template <int PROBE>
+// FX: B operand straight from fp32 X (split in registers) instead of the split
+// pass's XB records; X rows readable up to `pread` floats (>= P, % 4 == 0).
+template <int PROBE, bool FX>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void dense_split3_kernel(const uint8_t* __restrict__ WA, const uint8_t* __restrict__ XB, float* __restrict__ Y,
                          int64_t ldy, int M, int64_t P, int64_t Mp, int64_t Pp, int n_stages, int n_mt,
-                         int64_t n_pt, int64_t tiles_per_xcd, int group_m) {
+                         int64_t n_pt, int64_t tiles_per_xcd, int group_m, const float* __restrict__ X,
+                         int64_t ldx, int K, int64_t pread) {
+  constexpr int kStage = FX ? kStageFX : kStageBytes;
+  constexpr int kDma = FX ? kDmaFX : kDmaPerWave;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int64_t j = blockIdx.x >> 3;
   const int64_t t = (blockIdx.x & 7) * tiles_per_xcd + j;
@@ -169,10 +228,18 @@ void dense_split3_kernel(const uint8_t* __restrict__ WA, const uint8_t* __restri
   const int64_t pitchA = Mp * kRec, pitchB = Pp * kRec;  // bytes per k-group
   auto issue = [&](int s) {
     if constexpr (PROBE == 1) return;
-    uint8_t* st = lds + (s % kStages) * kStageBytes;
+    uint8_t* st = lds + (s % kStages) * kStage;
 #pragma unroll
-    for (int i = 0; i < kDmaPerWave; ++i) {
-      const int q = wave + 4 * i;      // 0..47, 1 KiB each
+    for (int i = 0; i < kDma; ++i) {
+      const int q = wave + 4 * i;      // 1 KiB each (A records) / one fp32 row of 256 p (FX B)
+      if (FX && q >= 24) {
+        const int k = min(16 * s + (q - 24), K - 1);     // rows past K: masked after the read
+        int64_t c = pt * kTile + lane * 4;
+        if (c + 4 > pread) c = pread - 4;                // columns past P: masked after the read
+        __builtin_amdgcn_global_load_lds(DOL_GPTR(X + int64_t(k) * ldx + c), DOL_LPTR(st + kOpStage + (q - 24) * kBPitch),
+                                         16, 0, 0);
+        continue;
+      }
       const int op = q / 24, qq = q % 24, kgl = qq / 12, chunk = qq % 12;
       const int64_t kg = 2 * int64_t(s) + kgl;
       const uint8_t* src = (op == 0 ? srcA + kg * pitchA : srcB + kg * pitchB) + chunk * 1024;
@@ -189,16 +256,35 @@ void dense_split3_kernel(const uint8_t* __restrict__ WA, const uint8_t* __restri
       for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
 
   auto read_frags = [&](int s, bf16x8 (&fa)[4][3], bf16x8 (&fb)[4][3]) {
-    const uint8_t* st = lds + (s % kStages) * kStageBytes;
+    const uint8_t* st = lds + (s % kStages) * kStage;
     const uint8_t* sa = st + h * (kTile * kRec) + (wm * 128 + li) * kRec;
-    const uint8_t* sb = st + kOpStage + h * (kTile * kRec) + (wn * 128 + li) * kRec;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int p = 0; p < 3; ++p) {
-        fa[i][p] = *reinterpret_cast<const bf16x8*>(sa + i * 32 * kRec + 16 * p);
-        fb[i][p] = *reinterpret_cast<const bf16x8*>(sb + i * 32 * kRec + 16 * p);
+      for (int p = 0; p < 3; ++p) fa[i][p] = *reinterpret_cast<const bf16x8*>(sa + i * 32 * kRec + 16 * p);
+    if constexpr (FX) {
+      const float* bs = reinterpret_cast<const float*>(st + kOpStage) + 8 * h * (kBPitch / 4);
+      const bool edge = (pt == n_pt - 1) || (16 * s + 16 > K);  // wave-uniform
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int pl = wn * 128 + i * 32 + li;
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = bs[j * (kBPitch / 4) + pl];
+        if (edge) {
+          const bool pin = pt * kTile + pl < P;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = (pin && 16 * s + 8 * h + j < K) ? v[j] : 0.f;
+        }
+        split8(v, fb[i][0], fb[i][1], fb[i][2]);
       }
+    } else {
+      const uint8_t* sb = st + kOpStage + h * (kTile * kRec) + (wn * 128 + li) * kRec;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) fb[i][p] = *reinterpret_cast<const bf16x8*>(sb + i * 32 * kRec + 16 * p);
+    }
   };
   // the six piece products of one 32x32x16 block, smallest first
   auto mfmas = [&](const bf16x8 (&fa)[4][3], const bf16x8 (&fb)[4][3]) {
@@ -226,7 +312,7 @@ void dense_split3_kernel(const uint8_t* __restrict__ WA, const uint8_t* __restri
   issue(0);
   if (n_stages > 1) issue(1);
   for (int s = 0; s < n_stages; ++s) {
-    wait_vmcnt_stage(s + 1 < n_stages);  // my DMA of stage s landed
+    wait_vmcnt_stage<FX>(s + 1 < n_stages);  // my DMA of stage s landed
     barrier();                           // ... and every wave's; stage (s + 2) % 3 is free
     if (s + 2 < n_stages) issue(s + 2);
     if constexpr (PROBE == 2) continue;
@@ -264,12 +350,26 @@ inline Split3Geom geom(int32_t M, int32_t K, int64_t P) {
   return g;
 }
 
+// The in-register X split (FX kernel, opt-in with DOL_SPLIT3_FUSE_X) needs whole
+// 16-B pieces of X rows: rows 16-B aligned, ldx % 4 == 0 and readable up to
+// round_up(P, 4) floats — always so when P % 4 == 0, and asserted by the caller
+// with DOL_SPLIT3_X_ROWS_PADDED.  It needs no X workspace (0.40 vs 5.4 GB at
+// 8192 x 101,770) but runs slower: 68.8 vs 54.4 ms there, 1.45 vs 1.43 ms at
+// 1024 agents (each B value is split by both row-waves, 32 ds_read_b32 + ~250
+// VALU per stage and wave beside the 96 MFMAs) — the split pass is the default.
+inline bool fused_x_ok(const float* X, int64_t ldx, int64_t P, int flags) {
+  const bool aligned = reinterpret_cast<uintptr_t>(X) % 16 == 0 && ldx % 4 == 0;
+  return (flags & DOL_SPLIT3_FUSE_X) && aligned && P >= 4 && (P % 4 == 0 || (flags & DOL_SPLIT3_X_ROWS_PADDED));
+}
+
 }  // namespace
 
-extern "C" int64_t dol_mix_dense_split3_workspace_bytes(int32_t M, int32_t K, int64_t P) {
+extern "C" int64_t dol_mix_dense_split3_workspace_bytes(int32_t M, int32_t K, int64_t P, int flags) {
   if (M <= 0 || K <= 0 || P <= 0) return 0;
   const Split3Geom g = geom(M, K, P);
-  return g.bytesA + g.bytesB;
+  // FUSE_X + X_ROWS_PADDED promise the fused path (given an aligned X): W pieces only
+  const bool fused = (flags & DOL_SPLIT3_FUSE_X) && (flags & DOL_SPLIT3_X_ROWS_PADDED) && P >= 4;
+  return fused ? g.bytesA : g.bytesA + g.bytesB;
 }
 
 extern "C" int dol_mix_dense_split3_f32(const float* W, int64_t ldw, const float* X, int64_t ldx, float* Y,
@@ -284,18 +384,20 @@ extern "C" int dol_mix_dense_split3_f32(const float* W, int64_t ldw, const float
   if (K == 0) return hipMemset2DAsync(Y, ldy * 4, 0, P * 4, M, s) == hipSuccess ? DOL_OK
                      : fail(DOL_EINVAL, "dol_mix_dense_split3_f32: memset failed");
   const Split3Geom g = geom(M, K, P);
-  if (!work || work_bytes < g.bytesA + g.bytesB)
+  const bool fx = fused_x_ok(X, ldx, P, flags);
+  const int64_t need = fx ? g.bytesA : g.bytesA + g.bytesB;
+  if (!work || work_bytes < need)
     return fail(DOL_EINVAL, "dol_mix_dense_split3_f32: workspace %lld bytes, need %lld",
-                static_cast<long long>(work_bytes), static_cast<long long>(g.bytesA + g.bytesB));
+                static_cast<long long>(work_bytes), static_cast<long long>(need));
   if (reinterpret_cast<uintptr_t>(work) % 256) return fail(DOL_EINVAL, "dol_mix_dense_split3_f32: workspace not 256-B aligned");
   uint8_t* wa = static_cast<uint8_t*>(work);
-  uint8_t* xb = wa + g.bytesA;
+  uint8_t* xb = fx ? nullptr : wa + g.bytesA;
   if (!(flags & DOL_SPLIT3_W_READY)) {
     const int64_t n = g.Mp * g.Kg;
     hipLaunchKernelGGL(split3_rows_kernel, dim3(static_cast<unsigned>(cdiv(n, 256))), dim3(256), 0, s, W, ldw, M, K,
                        static_cast<int>(g.Mp), static_cast<int>(g.Kg), wa);
   }
-  {
+  if (!fx) {
     const int64_t n = g.Pp * g.Kg;
     if (cdiv(n, 256) >= (int64_t(1) << 32)) return fail(DOL_EINVAL, "dol_mix_dense_split3_f32: X too large");
     hipLaunchKernelGGL(split3_cols_kernel, dim3(static_cast<unsigned>(cdiv(n, 256))), dim3(256), 0, s, X, ldx, K, P,
@@ -305,23 +407,28 @@ extern "C" int dol_mix_dense_split3_f32(const float* W, int64_t ldw, const float
   const int64_t n_pt = g.Pp / kTile;
   const int64_t tiles_per_xcd = cdiv(int64_t(n_mt) * n_pt, 8);
   if (8 * tiles_per_xcd >= (int64_t(1) << 32)) return fail(DOL_EINVAL, "dol_mix_dense_split3_f32: too many tiles");
-  static int probe = -1, group_m = kGroupM;
-  if (probe < 0) {
-    const char* e = getenv("DOL_SPLIT3_PROBE");
-    probe = e ? atoi(e) : 0;
-    const char* gm = getenv("DOL_SPLIT3_GROUP_M");
-    if (gm && atoi(gm) > 0) group_m = atoi(gm);
-    for (const void* k : {reinterpret_cast<const void*>(dense_split3_kernel<0>),
-                          reinterpret_cast<const void*>(dense_split3_kernel<1>),
-                          reinterpret_cast<const void*>(dense_split3_kernel<2>)})
-      (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
-  }
-  auto launch = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(8 * tiles_per_xcd)), dim3(256), kLds, s, wa, xb, Y, ldy, M,
-                       P, g.Mp, g.Pp, static_cast<int>(g.Kg / 2), n_mt, n_pt, tiles_per_xcd, group_m);
+  // diagnostics knobs (tools/gpu_dense_probe.sh); read once per process
+  static const int probe = [] { const char* e = getenv("DOL_SPLIT3_PROBE"); return e ? atoi(e) : 0; }();
+  static const int group_m = [] {
+    const char* e = getenv("DOL_SPLIT3_GROUP_M");
+    return e && atoi(e) > 0 ? atoi(e) : kGroupM;
+  }();
+  const int64_t pread = (P % 4 == 0) ? P : (P + 3) / 4 * 4;
+  auto launch = [&](auto kern, int lds) {
+    // > 64 KiB of dynamic LDS: set on every call (cheap), so every device of the process gets it
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(8 * tiles_per_xcd)), dim3(256), lds, s, wa, xb, Y, ldy, M,
+                       P, g.Mp, g.Pp, static_cast<int>(g.Kg / 2), n_mt, n_pt, tiles_per_xcd, group_m, X, ldx, K,
+                       pread);
   };
-  if (probe == 1) launch(dense_split3_kernel<1>);
-  else if (probe == 2) launch(dense_split3_kernel<2>);
-  else launch(dense_split3_kernel<0>);
+  if (fx) {
+    if (probe == 1) launch(dense_split3_kernel<1, true>, kStages * kStageFX);
+    else if (probe == 2) launch(dense_split3_kernel<2, true>, kStages * kStageFX);
+    else launch(dense_split3_kernel<0, true>, kStages * kStageFX);
+  } else {
+    if (probe == 1) launch(dense_split3_kernel<1, false>, kLds);
+    else if (probe == 2) launch(dense_split3_kernel<2, false>, kLds);
+    else launch(dense_split3_kernel<0, false>, kLds);
+  }
   return dol::check_launch("dol_mix_dense_split3_f32");
 }

@@ -370,11 +370,11 @@ class MixingPlan:
             return ops.mix_dense(self.W, X, Y, P=P)
         P = X.shape[1] if P is None else P
         M, K = self.W.shape
-        key = (M, K, int(P), X.device)
-        ready = self._work_key == key  # this plan's W already split into the workspace
+        need = ops.dense_split3_workspace_bytes(M, K, P, 0)
+        key = (M, K, X.device)
+        ready = self._work_key == key and self._work.numel() >= need  # W already split into the workspace
         if not ready:
-            self._work = torch.empty(max(ops.dense_split3_workspace_bytes(M, K, P), 1), dtype=torch.uint8,
-                                     device=X.device)
+            self._work = torch.empty(max(need, 1), dtype=torch.uint8, device=X.device)
         ops.mix_dense_split3(self.W, X, Y, P=P, work=self._work, w_ready=ready)
         self._work_key = key
         return Y

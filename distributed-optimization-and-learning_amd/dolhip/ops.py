@@ -14,7 +14,7 @@ from . import _native
 from ._native import DolNativeError
 
 __all__ = [
-    "DolNativeError", "mix_csr", "mix_ring", "mix_dense", "mix_dense_split3", "dense_split3_workspace_bytes",
+    "DolNativeError", "mix_csr", "mix_ring", "mix_dense", "mix_dense_split3", "dense_split3_workspace_bytes", "split3_x_flags",
     "mix_ring_steps", "prox_admm_sgd", "admm_dual", "ordered_mean",
     "ordered_sum", "stream_copy", "dual_workspace_bytes", "prox_grad", "admm_step_dual", "mlp_step",
     "dgd_ring", "dgd_csr", "OBJECTIVES",
@@ -190,17 +190,37 @@ def mix_dense(W: torch.Tensor, X: torch.Tensor, Y: torch.Tensor, P: Optional[int
     return Y
 
 
-def dense_split3_workspace_bytes(M: int, K: int, P: int) -> int:
-    return int(_native.lib().dol_mix_dense_split3_workspace_bytes(int(M), int(K), int(P)))
+SPLIT3_W_READY, SPLIT3_X_ROWS_PADDED, SPLIT3_FUSE_X = 1, 2, 4  # dol_hip.h flags
+
+
+def split3_x_flags(X: torch.Tensor, P: int) -> int:
+    """DOL_SPLIT3_X_ROWS_PADDED when the GEMM may read X's rows in whole 16-B
+    pieces up to round_up(P, 4) floats (aligned rows, ld % 4 == 0, storage
+    present): X is then split in registers, with no split pass."""
+    if X.data_ptr() % 16 or X.dim() != 2 or (X.shape[0] > 1 and X.stride(0) % 4):
+        return 0
+    ld = X.stride(0) if X.shape[0] > 1 else X.shape[1]
+    p4 = -(-P // 4) * 4
+    if ld < p4:
+        return 0
+    need = X.storage_offset() + (X.shape[0] - 1) * ld + p4
+    return SPLIT3_X_ROWS_PADDED if need * 4 <= X.untyped_storage().nbytes() else 0
+
+
+def dense_split3_workspace_bytes(M: int, K: int, P: int, flags: int = 0) -> int:
+    return int(_native.lib().dol_mix_dense_split3_workspace_bytes(int(M), int(K), int(P), int(flags)))
 
 
 def mix_dense_split3(W: torch.Tensor, X: torch.Tensor, Y: torch.Tensor, P: Optional[int] = None,
-                     work: Optional[torch.Tensor] = None, w_ready: bool = False) -> torch.Tensor:
+                     work: Optional[torch.Tensor] = None, w_ready: bool = False,
+                     fuse: bool = False) -> torch.Tensor:
     """Y = W X on the bf16 matrix cores at fp32 accuracy (dol_mix_dense_split3_f32:
     three-piece bf16 split of both operands, six piece products per term).
-    `work`: a uint8 device buffer of >= dense_split3_workspace_bytes(M, K, P)
-    bytes (allocated per call when None); w_ready=True reuses the split W that
-    a previous call with the same W left in `work`."""
+    fuse=True splits X inside the GEMM when its rows allow (no X workspace,
+    slower; same bits) instead of in a split pass.  `work`: a uint8 device
+    buffer of >= dense_split3_workspace_bytes(M, K, P, flags) bytes (allocated
+    per call when None); w_ready=True reuses the split W that a previous call
+    with the same W left in `work`."""
     P = X.shape[1] if P is None else P
     ldw = _check_rows("W", W)
     ldx = _check_rows("X", X, P)
@@ -210,7 +230,8 @@ def mix_dense_split3(W: torch.Tensor, X: torch.Tensor, Y: torch.Tensor, P: Optio
         raise ValueError(f"shapes: W {tuple(W.shape)}, X {tuple(X.shape)}, Y {tuple(Y.shape)}")
     if Y.data_ptr() in (X.data_ptr(), W.data_ptr()):
         raise ValueError("Y aliases an input")
-    need = dense_split3_workspace_bytes(M, K, P)
+    flags = ((SPLIT3_FUSE_X | split3_x_flags(X, P)) if fuse else 0) | (SPLIT3_W_READY if w_ready else 0)
+    need = dense_split3_workspace_bytes(M, K, P, flags)
     if work is None:
         if w_ready:
             raise ValueError("w_ready needs the workspace of the call that split W")
@@ -218,7 +239,7 @@ def mix_dense_split3(W: torch.Tensor, X: torch.Tensor, Y: torch.Tensor, P: Optio
     elif work.device != X.device or work.dtype != torch.uint8 or work.numel() < need:
         raise ValueError(f"work: need a uint8 tensor of >= {need} bytes on {X.device}")
     _native.call("dol_mix_dense_split3_f32", W.data_ptr(), ldw, X.data_ptr(), ldx, Y.data_ptr(), ldy, M, K, P,
-                 work.data_ptr(), work.numel(), 1 if w_ready else 0, _stream(X))
+                 work.data_ptr(), work.numel(), flags, _stream(X))
     return Y
 
 

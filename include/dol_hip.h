@@ -111,16 +111,25 @@ int dol_mix_dense_f32(const float* W, int64_t ldw, const float* X, int64_t ldx,
  * piece products summed on v_mfma_f32_32x32x16_bf16 in fp32: 2.67x the
  * exact-f32 MFMA rate.  Error: |Y - W.X| <= (gamma_{6K'} + 2^-23) sum|W||X|
  * with gamma in units of 2^-23 (K' = K rounded up to 16); tests state the
- * observed maximum.  Subnormal pieces (|value| < ~1e-33) may be flushed.
- * `work` (>= dol_mix_dense_split3_workspace_bytes(M, K, P), 256-B aligned)
- * receives the split operands; flags & DOL_SPLIT3_W_READY reuses the split W
- * a previous call left in `work` (same W, M, K, P).  Y must not alias W or X.
+ * observed maximum.  Finite inputs (0 * Inf of a dense GEMM gives NaN).
+ * A split pass writes X's pieces to `work`, then the GEMM runs.  With
+ * DOL_SPLIT3_FUSE_X (memory-lean, slower) X is instead split in registers
+ * inside the GEMM when its rows are 16-B aligned with ldx % 4 == 0 and readable
+ * in whole 16-B pieces (P % 4 == 0, or DOL_SPLIT3_X_ROWS_PADDED: every row
+ * readable up to round_up(P, 4) floats); both give the same bits.  `work`
+ * (>= dol_mix_dense_split3_workspace_bytes(M, K, P, flags), 256-B aligned)
+ * receives the split W (and X); flags & DOL_SPLIT3_W_READY reuses the split W
+ * a previous call left in `work` (same W, M, K).  Y must not alias W or X.
  */
 #define DOL_SPLIT3_W_READY 1
+#define DOL_SPLIT3_X_ROWS_PADDED 2
+#define DOL_SPLIT3_FUSE_X 4
 int dol_mix_dense_split3_f32(const float* W, int64_t ldw, const float* X, int64_t ldx,
                              float* Y, int64_t ldy, int32_t M, int32_t K, int64_t P,
                              void* work, int64_t work_bytes, int flags, hipStream_t s);
-int64_t dol_mix_dense_split3_workspace_bytes(int32_t M, int32_t K, int64_t P);
+/* Workspace bytes for dol_mix_dense_split3_f32 with these flags: the split W
+ * only when FUSE_X | X_ROWS_PADDED promise the fused path, else W + X. */
+int64_t dol_mix_dense_split3_workspace_bytes(int32_t M, int32_t K, int64_t P, int flags);
 
 /*
  * One round of decentralised gradient descent on a separable synthetic loss

@@ -391,7 +391,7 @@ def test_mix_dense_split3_matches_f32_kernel_and_ragged_rows(gpu):
     X = (rng.standard_normal((K, P)) * 10.0 ** rng.integers(-3, 4, (K, 1))).astype(np.float32)
     Wd, Xd = dev(W, gpu), dev(X, gpu)
     Y1, Y2, Y3 = (torch.empty(M, P, device=gpu) for _ in range(3))
-    work = torch.empty(ops.dense_split3_workspace_bytes(M, K, P), dtype=torch.uint8, device=gpu)
+    work = torch.empty(ops.dense_split3_workspace_bytes(M, K, P, 0), dtype=torch.uint8, device=gpu)
     ops.mix_dense_split3(Wd, Xd, Y1, work=work)
     ops.mix_dense_split3(Wd, Xd, Y2, work=work, w_ready=True)
     ops.mix_dense(Wd, Xd, Y3)
@@ -402,6 +402,36 @@ def test_mix_dense_split3_matches_f32_kernel_and_ragged_rows(gpu):
     e_f32 = np.abs(Y3.cpu().numpy() - want64)
     assert np.all(e_split <= _split3_bound(W, X) + 1e-30)
     assert e_split.max() <= 2 * e_f32.max() + 1e-30
+
+
+@pytest.mark.parametrize("M,K,P,extra", [(256, 256, 1024, 0), (130, 37, 1031, 1), (300, 600, 5000, 4),
+                                         (64, 20, 4, 0), (513, 300, 701, 3), (200, 50, 999, 0)])
+def test_mix_dense_split3_fused_x_equals_split_pass(M, K, P, extra, gpu):
+    """X split in registers inside the GEMM (rows 16-B readable) gives the same
+    bits as the split pass, at ragged K / P tiles, NaN padding past P, values
+    near the bf16 overflow threshold (the wave's scalar fallback), subnormals
+    and signed zeros; ld % 4 != 0 falls back to the split pass."""
+    rng = np.random.default_rng(M * 7 + K)
+    W = ((rng.random((M, K)) < 0.3) * rng.random((M, K))).astype(np.float32)
+    X = rng.standard_normal((K, P)).astype(np.float32)
+    X[0, :4] = [3.0e38, -3.3e38, 1e-40, -0.0]
+    if K > 3:
+        X[3, -1] = 3.3895e38
+    Wd, Xd = dev(W, gpu), padded(X, gpu, extra)
+    fused = ops.split3_x_flags(Xd, P) != 0
+    assert fused == (((P + extra) % 4 == 0) and P >= 4)
+    Y1, Y2 = padded(np.zeros((M, P), np.float32), gpu, extra), padded(np.zeros((M, P), np.float32), gpu, extra)
+    ops.mix_dense_split3(Wd, Xd, Y1, P=P, fuse=True)
+    ops.mix_dense_split3(Wd, Xd, Y2, P=P)
+    torch.cuda.synchronize()
+    a, b = Y1[:, :P].cpu().numpy(), Y2[:, :P].cpu().numpy()
+    assert bits_equal(a, b)
+    assert np.isnan(Y1[:, P:].cpu().numpy()).all()
+    want64 = W.astype(np.float64) @ X.astype(np.float64)
+    big = (W[:, 0] > 0) | ((W[:, 3] > 0) if K > 3 else False)
+    ok = ~big  # rows that do not touch the ~3e38 entries: inside the bound
+    err = np.abs(a[ok].astype(np.float64) - want64[ok])
+    assert np.all(err <= _split3_bound(W[ok], X) + 1e-30)
 
 
 def test_mix_dense_split3_argument_errors(gpu):

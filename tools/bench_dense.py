@@ -51,8 +51,11 @@ def main():
             Y1 = torch.empty_like(X)
             Y2 = torch.empty_like(X)
             flops = 2.0 * N * N * P
-            work = torch.empty(ops.dense_split3_workspace_bytes(N, N, P), dtype=torch.uint8, device=dev)
-            rec = {"agents": N, "params": P, "flop_per_round": flops, "workspace_GB": work.numel() / 1e9}
+            work = torch.empty(ops.dense_split3_workspace_bytes(N, N, P, 0), dtype=torch.uint8, device=dev)
+            rec = {"agents": N, "params": P, "flop_per_round": flops, "workspace_GB": work.numel() / 1e9,
+                   "workspace_fused_x_GB": ops.dense_split3_workspace_bytes(N, N, P, 6) / 1e9}
+            ms_u = timed(lambda: ops.mix_dense_split3(W, X, Y2, P=P, work=work, fuse=True), a.reps)
+            rec.update({"fused_x_ms": ms_u, "fused_x_TFLOPs": flops / ms_u / 1e9})
             ms_s = timed(lambda: ops.mix_dense_split3(W, X, Y2, P=P, work=work), a.reps)
             ms_g = timed(lambda: ops.mix_dense_split3(W, X, Y2, P=P, work=work, w_ready=True), a.reps)
             rec.update({"split3_ms": ms_s, "split3_TFLOPs": flops / ms_s / 1e9,
