@@ -194,7 +194,10 @@ __device__ __forceinline__ void split8(const float (&v)[8], bf16x8& p0, bf16x8& 
 // staging-only 20 ms.  Tried and dropped (same box, no gain): fragments
 // double-buffered in registers with the DMA three stages ahead; the
 // v_mfma_f32_16x16x32_bf16 shape with (k-group, piece pair) k slots (same
-// speed, and mixing piece scales inside one MFMA loses exactness of x0+x1+x2).
+// speed, and mixing piece scales inside one MFMA loses exactness of x0+x1+x2);
+// the DMA issue sliced between the row blocks' MFMA clusters (sched_barrier
+// fenced; 53.5-54.1 vs 53.6-53.7 ms).  The full kernel's gap to the MFMA-only
+// probe is not an issue-order effect.
 // FX: B operand straight from fp32 X (split in registers) instead of the split
 // pass's XB records; X rows readable up to `pread` floats (>= P, % 4 == 0).
 template <int PROBE, bool FX>
