@@ -365,6 +365,7 @@ def main():
                 "algorithmic_bytes_per_launch": alg_bytes,
                 "kernel_ms": kern_ms,
                 "copy_kernel_GBps": copy_gbps,
+                "frac_of_measured_copy": (achieved / copy_gbps) if copy_gbps else None,
             },
             "cpu_baseline": cpu,
             "primal_dual_round": pd_round,

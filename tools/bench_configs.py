@@ -203,6 +203,8 @@ def main():
                    "rounds_per_launch": steps, "ms_per_launch": ms, "rounds_per_s": steps * 1e3 / ms,
                    "GBps": alg / (ms / 1e3) / 1e9, "frac_of_8TBps": alg / (ms / 1e3) / 1e9 / 8000.0,
                    "plan_build_s": build_s}
+            if plan.kind == "csr":  # the naive (nnz + N) * P * 4 figure beside the 2 * N * P * 4 one
+                rec["GBps_naive_nnz_plus_n"] = (plan.csr.nnz + N) * P * 4 / (ms / 1e3) / 1e9
             if "flops" in extra:
                 tf = extra["flops"] / (ms / 1e3) / 1e12
                 rec.update({"TFLOPs": tf, "mfma_util_vs_157TF": tf / 157.3})
