@@ -395,7 +395,9 @@ __global__ __launch_bounds__(kThreads) void csr_mix_kernel(
 // slabs re-read through the Infinity Cache.  Degree-4 rows (random-regular)
 // gather all passes' indices before any neighbour load (16.68 vs 16.80 ms).
 // A persistent variant (a fixed grid per XCD walking the tiles in step, so
-// only one slab is live in L2) ran 25-46 ms: latency-bound, dropped.
+// only one slab is live in L2) ran 25-46 ms: latency-bound, dropped.  Tile
+// widths (same box, 8192 x 2^20): 512 B 16.7 ms, 384 B (240-thread blocks)
+// 22.6 ms, 256 B 18.2 ms.
 template <int W, int PASSES, class Epi = NoEpi>
 __global__ __launch_bounds__(kThreads) void csr_xcd_kernel(
     const float* __restrict__ X, int64_t ldx, float* __restrict__ Y, int64_t ldy, int n_rows,
@@ -928,22 +930,23 @@ int mix_csr_impl(const char* nm, const float* X, int64_t ldx, int32_t x_rows, fl
     return fail(DOL_EINVAL, "%s: problem too large for one launch", nm);
   int64_t done4 = 0;
   if (use_xcd) {
-    const int64_t ntiles = cs.n4 / XW;
     const int passes = env_int("DOL_CSR_PASSES", XPASSES);
     auto go = [&](auto pc) {
       constexpr int PS = decltype(pc)::value;
+      const int64_t nt = cs.n4 / XW;
       const int64_t nrb = cdiv(n_rows, (kThreads / XW) * PS);
-      const int64_t grid = cdiv(ntiles, 8) * 8 * nrb;
+      const int64_t grid = cdiv(nt, 8) * 8 * nrb;
       if (grid > kMaxBlocks * 8) return false;
       hipLaunchKernelGGL((csr_xcd_kernel<XW, PS, Epi>), dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, s, X,
-                         ldx, Y, ldy, n_rows, static_cast<uint32_t>(nrb), static_cast<uint32_t>(ntiles), rowptr, col,
+                         ldx, Y, ldy, n_rows, static_cast<uint32_t>(nrb), static_cast<uint32_t>(nt), rowptr, col,
                          val, epi);
+      done4 = nt * XW;
       return true;
     };
-    const bool ok = passes == 1 ? go(std::integral_constant<int, 1>{})
-                    : passes == 4 ? go(std::integral_constant<int, 4>{}) : go(std::integral_constant<int, XPASSES>{});
+    using std::integral_constant;
+    const bool ok = passes == 1 ? go(integral_constant<int, 1>{})
+                    : passes == 4 ? go(integral_constant<int, 4>{}) : go(integral_constant<int, XPASSES>{});
     if (!ok) return fail(DOL_EINVAL, "%s: problem too large for one launch", nm);
-    done4 = ntiles * XW;
   }
   if (cs.n4 > done4)  // column offset through c_off so the epilogue sees absolute columns
     launch_csr<f4, RPB, Epi>(X, ldx, Y, ldy, n_rows, done4 * 4, cs.n4 - done4, rowptr, col, val, s, epi);
