@@ -397,6 +397,7 @@ extern "C" int dol_mix_dense_split3_f32(const float* W, int64_t ldw, const float
   uint8_t* xb = fx ? nullptr : wa + g.bytesA;
   if (!(flags & DOL_SPLIT3_W_READY)) {
     const int64_t n = g.Mp * g.Kg;
+    if (cdiv(n, 256) >= (int64_t(1) << 32)) return fail(DOL_EINVAL, "dol_mix_dense_split3_f32: W too large");
     hipLaunchKernelGGL(split3_rows_kernel, dim3(static_cast<unsigned>(cdiv(n, 256))), dim3(256), 0, s, W, ldw, M, K,
                        static_cast<int>(g.Mp), static_cast<int>(g.Kg), wa);
   }
