@@ -67,11 +67,21 @@ class Simulator(object):
             return G.communication_csr(topology, mode, n, **kw)
         return G.communication_graph(topology, mode, n, verbose=bool(self.args.verbose), **kw)
 
+    DENSE_AUTO_MIN_AGENTS, DENSE_AUTO_MIN_DENSITY = 256, 0.05
+
     def plan(self, t: int) -> G.MixingPlan:
+        """Device plan of W[t]: ring / CSR (bit-exact, default).  args.dense_mixing
+        = True (or "auto": density >= 5 % and >= 256 agents) selects the dense
+        matrix-core GEMM instead (split3 bf16 MFMA, fp32-accurate tolerance path),
+        the fast choice for complete / dense Erdos-Renyi graphs at scale."""
         p = self._plans.get(t)
         if p is None:
             g = self.adjacent_matrix[t]
-            p = G.MixingPlan(g, self.device) if isinstance(g, G.CSR) else G.MixingPlan.from_graph(g, self.device)
+            csr = g if isinstance(g, G.CSR) else G.csr_from_dense(g)
+            dm = self.args.dense_mixing
+            dense = bool(dm) if dm != "auto" else (csr.n_rows >= self.DENSE_AUTO_MIN_AGENTS and
+                                                   csr.nnz >= self.DENSE_AUTO_MIN_DENSITY * csr.n_rows * csr.n_cols)
+            p = G.MixingPlan(csr, self.device, dense=dense)
             self._plans[t] = p
         return p
 

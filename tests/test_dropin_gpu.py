@@ -187,6 +187,26 @@ def test_sparse_graphs_simulator_matches_dense(gpu):
     assert oracle.bits_equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize("dense_mixing", [True, "auto"])
+def test_dense_mixing_option_matches_csr(dense_mixing, gpu):
+    """args.dense_mixing routes a complete-graph W[t] to the split3 matrix-core
+    GEMM; the mixed parameters stay within fp32 accuracy of the bit-exact CSR
+    mix (|d| <= 1e-5 * max|x|; observed ~1e-7 relative)."""
+    m = load_project("weighted_average", ["simulators", "utils"])
+    outs = []
+    for dm in (None, dense_mixing):
+        torch.manual_seed(2028)
+        args = _small_dist_args(m["utils"], topology="compelete", dense_mixing=dm, num_users=40)
+        sim = m["simulators"].DecFedAvg(args)
+        sim.DENSE_AUTO_MIN_AGENTS = 32  # "auto" at test size
+        assert sim.plan(0).kind == ("csr" if dm is None else "dense")
+        for t in range(2):
+            sim.mix(t % len(sim.adjacent_matrix))
+        outs.append(sim.bank.rows().cpu().numpy())
+    scale = np.abs(outs[0]).max()
+    assert np.abs(outs[0] - outs[1]).max() <= 1e-5 * scale
+
+
 @pytest.mark.parametrize("key", sorted(TRAJ["dist_variants"]))
 def test_gossip_variant_trajectories_match_reference(key, gpu):
     """Other topologies (star / complete / dynamic with its NaN rows / Sinkhorn
