@@ -287,8 +287,9 @@ def main():
     fedlcon = None
     if world == 1 and not args.no_primal_dual:
         from dolhip import ops as _ops
-        eps, reps = 5, 5
-        _ops.mix_ring_steps(ring.x, ring.y, ring.w_prev, ring.w_next, eps, P=P, n_rows=N)
+        eps, reps = 5, 10
+        for _ in range(2):
+            _ops.mix_ring_steps(ring.x, ring.y, ring.w_prev, ring.w_next, eps, P=P, n_rows=N)
         torch.cuda.synchronize(device)
         s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s_ev.record()

@@ -89,6 +89,8 @@ __device__ __forceinline__ f4 axpy0(float wp, f4 a, float wn, f4 b) {
   return f4{axpy0(wp, a.x, wn, b.x), axpy0(wp, a.y, wn, b.y),
             axpy0(wp, a.z, wn, b.z), axpy0(wp, a.w, wn, b.w)};
 }
+// (ring_steps_kernel with 8-B lanes and R = 22-54: 11.25-11.65 ms vs 11.24-11.27
+// for f4 / R = 22 at eps = 5, 8192 x 2^20, same box: kept f4)
 __device__ __forceinline__ float fmac(float acc, float a, float x) { return acc + a * x; }
 __device__ __forceinline__ f4 fmac(f4 acc, float a, f4 x) {
   return f4{acc.x + a * x.x, acc.y + a * x.y, acc.z + a * x.z, acc.w + a * x.w};
@@ -301,7 +303,7 @@ __global__ __launch_bounds__(kThreads) void ring_mix_dma_kernel(
 // result is bit-identical to STEPS launches of ring_mix_kernel.  Wrap-around
 // ring inside X (one shard).
 // ----------------------------------------------------------------------------
-template <int STEPS, int R>
+template <int STEPS, int R, typename V = f4>
 __global__ __launch_bounds__(kThreads) void ring_steps_kernel(
     const float* __restrict__ X, int64_t ldx, float* __restrict__ Y, int64_t ldy, int n_rows,
     int64_t ncols_v, uint32_t n_col_tiles, const float* __restrict__ wprev,
@@ -321,16 +323,16 @@ __global__ __launch_bounds__(kThreads) void ring_steps_kernel(
   const int64_t c = int64_t(ct) * kThreads + threadIdx.x;
   if (c >= ncols_v) return;
   auto wrap = [&](int r) { r %= n_rows; return r < 0 ? r + n_rows : r; };
-  f4 v[L];
+  V v[L];
 #pragma unroll
-  for (int i = 0; i < L; ++i) v[i] = reinterpret_cast<const f4*>(X + int64_t(wrap(r0 - STEPS + i)) * ldx)[c];
+  for (int i = 0; i < L; ++i) v[i] = reinterpret_cast<const V*>(X + int64_t(wrap(r0 - STEPS + i)) * ldx)[c];
 #pragma unroll
   for (int t = 1; t <= STEPS; ++t) {
-    f4 prev_old = v[t - 1];
+    V prev_old = v[t - 1];
 #pragma unroll
     for (int i = t; i < L - t; ++i) {
       const int g = wrap(r0 - STEPS + i);
-      const f4 cur_old = v[i];
+      const V cur_old = v[i];
       v[i] = axpy0(wprev[g], prev_old, wnext[g], v[i + 1]);
       prev_old = cur_old;
     }
@@ -338,7 +340,7 @@ __global__ __launch_bounds__(kThreads) void ring_steps_kernel(
 #pragma unroll
   for (int i = 0; i < R; ++i) {
     const int r = r0 + i;
-    if (r < n_rows) __builtin_nontemporal_store(v[STEPS + i], reinterpret_cast<f4*>(Y + int64_t(r) * ldy) + c);
+    if (r < n_rows) __builtin_nontemporal_store(v[STEPS + i], reinterpret_cast<V*>(Y + int64_t(r) * ldy) + c);
   }
 }
 
@@ -1130,17 +1132,20 @@ int dol_mix_ring_steps_f32(const float* X, int64_t ldx, float* Y, int64_t ldy, i
   if (steps == 0) return fail(DOL_EINVAL, "dol_mix_ring_steps_f32: steps must be >= 1");
   const bool vec = row_vec_ok(X, ldx) && row_vec_ok(Y, ldy) && P % 4 == 0;
   if (!vec || steps > 8) return fail(DOL_EINVAL, "dol_mix_ring_steps_f32: needs 16-B aligned rows, P %% 4 == 0 and steps <= 8 (compose launches otherwise)");
-  const int64_t n4 = P / 4;
-  const uint32_t nct = static_cast<uint32_t>(cdiv(n4, kThreads));
-  auto go = [&](auto steps_c, auto r_c) {
+  auto go_v = [&](auto steps_c, auto r_c, auto v_c) {
     constexpr int S = decltype(steps_c)::value, R = decltype(r_c)::value;
+    using V = typename decltype(v_c)::type;
+    const int64_t nv = P / Vec<V>::W;
+    const uint32_t nct = static_cast<uint32_t>(cdiv(nv, kThreads));
     const int64_t nrt = cdiv(n_rows, R);
     const int64_t grid = cdiv(nct, 8) * 8 * nrt;
     if (grid > kMaxBlocks) return fail(DOL_EINVAL, "dol_mix_ring_steps_f32: too large");
-    hipLaunchKernelGGL((ring_steps_kernel<S, R>), dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, s, X, ldx, Y, ldy,
-                       n_rows, n4, nct, w_prev, w_next, static_cast<uint32_t>(nrt));
+    hipLaunchKernelGGL((ring_steps_kernel<S, R, V>), dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, s, X, ldx, Y,
+                       ldy, n_rows, nv, nct, w_prev, w_next, static_cast<uint32_t>(nrt));
     return check_launch("dol_mix_ring_steps_f32");
   };
+  struct TF4 { using type = f4; };
+  auto go = [&](auto steps_c, auto r_c) { return go_v(steps_c, r_c, TF4{}); };
   using std::integral_constant;
   // tile heights measured at 8192 x 2^20 (tools/bench_configs.py ring-eps<S>):
   // R = 6 for S <= 3, 14 for S = 4, 22 for S = 5-6, 30 for S = 7-8
