@@ -197,7 +197,9 @@ __device__ __forceinline__ void split8(const float (&v)[8], bf16x8& p0, bf16x8& 
 // speed, and mixing piece scales inside one MFMA loses exactness of x0+x1+x2);
 // the DMA issue sliced between the row blocks' MFMA clusters (sched_barrier
 // fenced; 53.5-54.1 vs 53.6-53.7 ms).  The full kernel's gap to the MFMA-only
-// probe is not an issue-order effect.
+// probe is not an issue-order effect.  128-row tiles (2 stages, two
+// workgroups per CU; or 3 stages): 1.27 / 1.40 vs 1.30 ms at 1024 agents,
+// 69-70 vs 58 ms at 8192 (profiles/r01c_dense_split3_tiles.txt): kept 256.
 // FX: B operand straight from fp32 X (split in registers) instead of the split
 // pass's XB records; X rows readable up to `pread` floats (>= P, % 4 == 0).
 template <int PROBE, bool FX>
