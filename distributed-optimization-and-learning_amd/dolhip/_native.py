@@ -55,6 +55,7 @@ SIGNATURES = {
     "dol_mlp_step_lds_bytes": [_i32, _i32, _i32],
     "dol_mix_dense_split3_f32": [_ptr, _i64, _ptr, _i64, _ptr, _i64, _i32, _i32, _i64, _ptr, _i64, ctypes.c_int, _ptr],
     "dol_mix_dense_split3_workspace_bytes": [_i32, _i32, _i64, ctypes.c_int],
+    "dol_er_stochastic_f32": [_ptr, _i64, _i32, _f32, ctypes.c_uint64, _ptr],
 }
 _RESTYPES = {"dol_last_error": ctypes.c_char_p, "dol_admm_dual_workspace_bytes": ctypes.c_int64,
              "dol_mlp_step_lds_bytes": ctypes.c_int64, "dol_mlp_step_workspace_bytes": ctypes.c_int64,

@@ -305,6 +305,17 @@ def erdos_renyi_stochastic(n: int, p: float, generator: torch.Generator, device=
     return torch.where(W > 0, W, torch.zeros((), dtype=W.dtype, device=dev))
 
 
+def erdos_renyi_stochastic_hip(n: int, p: float, seed: int, device, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """The same kind of W as erdos_renyi_stochastic (undirected G(n, p), zero
+    diagonal, 'stochastic' weighting, rows summing to 1), drawn by ONE HIP
+    kernel from a counter-based hash keyed by `seed` (dol_er_stochastic_f32)
+    instead of nine torch kernels: config 5's per-round W draw.  Not the
+    torch generator's stream."""
+    from . import ops
+    W = out if out is not None else torch.empty(n, n, dtype=torch.float32, device=device)
+    return ops.er_stochastic(W, p, seed)
+
+
 class MixingPlan:
     """Device form of one W: CSR tensors plus the ring specialisation if it applies."""
 

@@ -14,7 +14,7 @@ from . import _native
 from ._native import DolNativeError
 
 __all__ = [
-    "DolNativeError", "mix_csr", "mix_ring", "mix_dense", "mix_dense_split3", "dense_split3_workspace_bytes", "split3_x_flags",
+    "DolNativeError", "mix_csr", "mix_ring", "mix_dense", "mix_dense_split3", "dense_split3_workspace_bytes", "split3_x_flags", "er_stochastic",
     "mix_ring_steps", "prox_admm_sgd", "admm_dual", "ordered_mean",
     "ordered_sum", "stream_copy", "dual_workspace_bytes", "prox_grad", "admm_step_dual", "mlp_step",
     "dgd_ring", "dgd_csr", "OBJECTIVES",
@@ -241,6 +241,17 @@ def mix_dense_split3(W: torch.Tensor, X: torch.Tensor, Y: torch.Tensor, P: Optio
     _native.call("dol_mix_dense_split3_f32", W.data_ptr(), ldw, X.data_ptr(), ldx, Y.data_ptr(), ldy, M, K, P,
                  work.data_ptr(), work.numel(), flags, _stream(X))
     return Y
+
+
+def er_stochastic(W: torch.Tensor, p: float, seed: int) -> torch.Tensor:
+    """W[n, >=n] <- a fresh Erdos-Renyi G(n, p) mixing matrix under the
+    reference's 'stochastic' weighting, in one kernel (dol_er_stochastic_f32)."""
+    ld = _check_rows("W", W)
+    n = W.shape[0]
+    if W.shape[1] < n:
+        raise ValueError(f"W: expected [n, >= n], got {tuple(W.shape)}")
+    _native.call("dol_er_stochastic_f32", W.data_ptr(), ld, n, float(p), int(seed) & (2**64 - 1), _stream(W))
+    return W
 
 
 def mix_ring(X: torch.Tensor, Y: torch.Tensor, w_prev: torch.Tensor, w_next: torch.Tensor,

@@ -266,6 +266,17 @@ int64_t dol_mlp_step_workspace_bytes(int32_t n_agents, int32_t B, int32_t h);
 /* Dynamic LDS bytes the MLP step uses per workgroup (one agent). */
 int64_t dol_mlp_step_lds_bytes(int32_t B, int32_t h, int32_t c);
 
+/*
+ * A fresh Erdos-Renyi G(n, p) mixing matrix under the reference's 'stochastic'
+ * weighting (DIST/simulators.py:65-70: G = R o A, G /= colsum(G), W = G^T), A
+ * undirected with a zero diagonal, for BASELINE config 5's time-varying dense
+ * W — one kernel, W written once (rows sum to 1; entries the reference's
+ * Neighbors would drop, incl. empty columns, are 0).  Seeded and
+ * deterministic (counter-based hash; not torch's generator stream).
+ * W row-major [n][ldw], ldw >= n, n <= 65535, 0 <= p <= 1.
+ */
+int dol_er_stochastic_f32(float* W, int64_t ldw, int32_t n, float p, uint64_t seed, hipStream_t s);
+
 /* Streaming copy dst = src (n floats): HBM calibration kernel for roofline. */
 int dol_stream_copy_f32(const float* src, float* dst, int64_t n, hipStream_t s);
 

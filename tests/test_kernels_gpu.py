@@ -434,6 +434,73 @@ def test_mix_dense_split3_fused_x_equals_split_pass(M, K, P, extra, gpu):
     assert np.all(err <= _split3_bound(W[ok], X) + 1e-30)
 
 
+def _er_hip_numpy(n, p, seed):
+    """numpy restatement of graph_draw.hip (hash, keys, G = R o A, W = (G / colsum)^T)."""
+    M64 = (1 << 64) - 1
+
+    def splitmix(z):
+        z = (z + 0x9E3779B97F4A7C15) & M64
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M64
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M64
+        return z ^ (z >> 31)
+
+    h = splitmix(seed)
+    k_edge, k_w = np.uint32(h & 0xFFFFFFFF), np.uint32(((h >> 32) ^ 0x5BD1E995) & 0xFFFFFFFF)
+
+    def mix32(x):
+        x = x ^ (x >> np.uint32(16))
+        x = x * np.uint32(0x7FEB352D)
+        x = x ^ (x >> np.uint32(15))
+        x = x * np.uint32(0x846CA68B)
+        return x ^ (x >> np.uint32(16))
+
+    def u01(key, idx):
+        with np.errstate(over="ignore"):
+            return (mix32(idx * np.uint32(0x9E3779B9) + key) >> np.uint32(8)).astype(np.float32) * np.float32(2.0 ** -24)
+
+    i, j = np.meshgrid(np.arange(n, dtype=np.uint32), np.arange(n, dtype=np.uint32), indexing="ij")
+    a, b = np.minimum(i, j), np.maximum(i, j)
+    with np.errstate(over="ignore"):
+        edge = (u01(k_edge, a * np.uint32(n) + b) < np.float32(p)) & (i != j)
+        g = np.where(edge, u01(k_w, i * np.uint32(n) + j), np.float32(0))
+    with np.errstate(invalid="ignore", divide="ignore"):
+        W = (g / g.sum(0, dtype=np.float64).astype(np.float32)).T
+    return np.where(W > 0, W, 0).astype(np.float32)
+
+
+@pytest.mark.parametrize("n,p", [(1, 0.5), (7, 0.3), (257, 0.1), (1000, 0.02), (64, 0.0), (64, 1.0)])
+def test_er_stochastic_hip_structure(n, p, gpu):
+    """Config 5's per-round W drawn by one kernel: undirected G(n, p) pattern
+    with a zero diagonal, rows summing to 1 (empty rows all zero), edge density
+    within 5 sigma of p, deterministic per seed, and equal to a numpy
+    restatement of the kernel's hash (pattern exactly, values to 2 ulp-ish:
+    the colsum order differs)."""
+    W = G.erdos_renyi_stochastic_hip(n, p, 11, gpu)
+    W2 = G.erdos_renyi_stochastic_hip(n, p, 11, gpu)
+    W3 = G.erdos_renyi_stochastic_hip(n, p, 12, gpu)
+    torch.cuda.synchronize()
+    Wn = W.cpu().numpy()
+    assert bits_equal(Wn, W2.cpu().numpy())
+    if n > 8 and 0 < p < 1:
+        assert not np.array_equal(Wn, W3.cpu().numpy())
+    assert (np.diag(Wn) == 0).all() and np.isfinite(Wn).all()
+    A = Wn > 0
+    assert (A == A.T).all()
+    rs = Wn.astype(np.float64).sum(1)
+    has = A.any(1)
+    assert np.allclose(rs[has], 1.0, atol=2e-6) and (Wn[~has] == 0).all()
+    if p == 1.0:
+        assert (A == ~np.eye(n, dtype=bool)).all()
+    if p == 0.0:
+        assert not A.any()
+    if n >= 257 and 0 < p < 1:
+        m = n * (n - 1) / 2
+        assert abs(A.sum() / 2 / m - p) <= 5 * np.sqrt(p * (1 - p) / m)
+    want = _er_hip_numpy(n, p, 11)
+    assert ((want > 0) == A).all()
+    np.testing.assert_allclose(Wn, want, rtol=1e-6, atol=0)
+
+
 def test_mix_dense_split3_argument_errors(gpu):
     W = torch.zeros(8, 8, device=gpu)
     X = torch.zeros(8, 16, device=gpu)

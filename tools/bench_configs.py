@@ -34,7 +34,7 @@ def time_plan(plan, X, Y, P, reps):
 
 def mlp_round(N, d, h, c, B, p_edge, reps, dev):
     """BASELINE config 5: a NEW Erdos-Renyi W every round (drawn on the device,
-    graph.erdos_renyi_stochastic), mixed on the dense fp32 MFMA path, then one
+    graph.erdos_renyi_stochastic_hip), mixed on the dense matrix-core path, then one
     fused local step of every agent's MLP (dol_mlp_step_f32)."""
     from dolhip.bank import AgentBank
     from dolhip.mlp import BatchedMLP, mlp_layout
@@ -44,10 +44,12 @@ def mlp_round(N, d, h, c, B, p_edge, reps, dev):
     bank.buffer("y").zero_()
     bank.buffer("mom", zero=True)
     gen = torch.Generator(device=dev).manual_seed(2028)
-    state = {}
+    state = {"round": 0, "W": torch.empty(N, N, device=dev)}
 
-    def draw():
-        state["plan"] = G.MixingPlan.from_dense(G.erdos_renyi_stochastic(N, p_edge, gen))
+    def draw():  # a new W every round: one HIP kernel (graph_draw.hip), seeded per round
+        state["round"] += 1
+        W = G.erdos_renyi_stochastic_hip(N, p_edge, 2028 * 1000003 + state["round"], dev, out=state["W"])
+        state["plan"] = G.MixingPlan.from_dense(W)
     X = torch.randn(N, B, d, device=dev)
     y = torch.randint(0, c, (N, B), device=dev)
     ev = {k: [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
@@ -87,6 +89,15 @@ def mlp_round(N, d, h, c, B, p_edge, reps, dev):
     e_.record()
     torch.cuda.synchronize()
     ms["local_unfused"] = s_.elapsed_time(e_) / reps
+    # the torch form of the same draw (nine kernels), for comparison
+    G.erdos_renyi_stochastic(N, p_edge, gen)
+    torch.cuda.synchronize()
+    s_.record()
+    for _ in range(reps):
+        G.erdos_renyi_stochastic(N, p_edge, gen)
+    e_.record()
+    torch.cuda.synchronize()
+    ms["graph_torch"] = s_.elapsed_time(e_) / reps
 
     P = bank.P
     flops_fb = 2.0 * N * B * (d * h + h * c) * 3  # fwd + two backward GEMMs per layer
