@@ -189,7 +189,8 @@ __device__ __forceinline__ void split8(const float (&v)[8], bf16x8& p0, bf16x8& 
 }
 
 // PROBE (tools only, DOL_SPLIT3_PROBE): 1 = no operand staging (MFMA ceiling of
-// the loop), 2 = staging only (no fragment reads / MFMAs).  Measured at 8192 x
+// the loop), 2 = staging only (no fragment reads / MFMAs), 3 = as 1 without
+// the output stores, 4 = full kernel without the output stores.  Measured at 8192 x
 // 101770 (profiles/r01c_dense_split3_probe.txt): full 53 ms, MFMA-only 45 ms,
 // staging-only 20 ms.  Tried and dropped (same box, no gain): fragments
 // double-buffered in registers with the DMA three stages ahead; the
@@ -232,7 +233,7 @@ void dense_split3_kernel(const uint8_t* __restrict__ WA, const uint8_t* __restri
   const uint8_t* srcB = XB + pt * kTile * kRec + lane * 16;
   const int64_t pitchA = Mp * kRec, pitchB = Pp * kRec;  // bytes per k-group
   auto issue = [&](int s) {
-    if constexpr (PROBE == 1) return;
+    if constexpr (PROBE == 1 || PROBE == 3) return;
     uint8_t* st = lds + (s % kStages) * kStage;
 #pragma unroll
     for (int i = 0; i < kDma; ++i) {
@@ -334,7 +335,8 @@ void dense_split3_kernel(const uint8_t* __restrict__ WA, const uint8_t* __restri
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int row = mt * kTile + wm * 128 + a * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-        if (row < M && col < P) __builtin_nontemporal_store(acc[a][b][e], Y + int64_t(row) * ldy + col);
+        if (row < M && col < P && (PROBE < 3 || M < 0))  // probes 3/4 drop the stores (M < 0 never holds)
+          __builtin_nontemporal_store(acc[a][b][e], Y + int64_t(row) * ldy + col);
       }
     }
 }
@@ -434,6 +436,8 @@ extern "C" int dol_mix_dense_split3_f32(const float* W, int64_t ldw, const float
   } else {
     if (probe == 1) launch(dense_split3_kernel<1, false>, kLds);
     else if (probe == 2) launch(dense_split3_kernel<2, false>, kLds);
+    else if (probe == 3) launch(dense_split3_kernel<3, false>, kLds);
+    else if (probe == 4) launch(dense_split3_kernel<4, false>, kLds);
     else launch(dense_split3_kernel<0, false>, kLds);
   }
   return dol::check_launch("dol_mix_dense_split3_f32");
