@@ -47,6 +47,27 @@ def test_argument_errors_are_reported_without_launch():
     rc = L.dol_ordered_mean_f32(None, 4, None, 0, 4, None, None)
     assert rc == -1 and b"m must be >= 1" in L.dol_last_error()
     assert L.dol_admm_dual_workspace_bytes(4, 1 << 20) > 0
+    fake = 1 << 20  # never dereferenced: every call below fails its argument check first
+    rc = L.dol_er_stochastic_f32(fake, 100, 100, 1.5, 7, None)
+    assert rc == -1 and b"p outside" in L.dol_last_error()
+    rc = L.dol_er_stochastic_f32(fake, 70000, 70000, 0.1, 7, None)
+    assert rc == -1 and b"65535" in L.dol_last_error()
+    rc = L.dol_er_stochastic_f32(fake, 10, 100, 0.1, 7, None)
+    assert rc == -1 and b"ldw" in L.dol_last_error()
+    rc = L.dol_mix_dense_split3_f32(fake, 8, fake + 4096, 8, fake, 8, 8, 8, 8, fake, 1 << 30, 0, None)
+    assert rc == -1 and b"alias" in L.dol_last_error()
+    rc = L.dol_mix_dense_split3_f32(fake, 8, fake + 4096, 8, fake + 8192, 8, 8, 8, 8, fake, 16, 0, None)
+    assert rc == -1 and b"workspace" in L.dol_last_error()
+
+
+def test_split3_workspace_sizes():
+    L = _native.lib()
+    full = L.dol_mix_dense_split3_workspace_bytes(1024, 1024, 101770, 0)
+    lean = L.dol_mix_dense_split3_workspace_bytes(1024, 1024, 101770, 2 | 4)  # X_ROWS_PADDED | FUSE_X
+    # W pieces: Kg x Mp x 48 B; X pieces: Kg x Pp x 48 B (Kg = K/8, rows / columns padded to 256)
+    assert lean == 128 * 1024 * 48
+    assert full == lean + 128 * 101888 * 48
+    assert L.dol_mix_dense_split3_workspace_bytes(0, 5, 5, 0) == 0
 
 
 def test_cpu_tensors_are_refused():
