@@ -397,7 +397,11 @@ __global__ __launch_bounds__(kThreads) void csr_mix_kernel(
 // slabs re-read through the Infinity Cache.  Degree-4 rows (random-regular)
 // gather all passes' indices before any neighbour load (16.68 vs 16.80 ms).
 // A persistent variant (a fixed grid per XCD walking the tiles in step, so
-// only one slab is live in L2) ran 25-46 ms: latency-bound, dropped.  Tile
+// only one slab is live in L2) ran 25-46 ms: latency-bound, dropped.  A
+// persistent sweep (each workgroup holding 64 rows' partial sums in LDS, every
+// row group's neighbour lists merged into one j-ascending list, so all readers
+// of a line touch it together) was bit-exact but ran 27 ms with either tile
+// order (profiles/r01d_csr_sweep_kernel.txt), dropped.  Tile
 // widths (same box, 8192 x 2^20): 512 B 16.7 ms, 384 B (240-thread blocks)
 // 22.6 ms, 256 B 18.2 ms.
 template <int W, int PASSES, class Epi = NoEpi>
