@@ -133,10 +133,12 @@ __global__ __launch_bounds__(256) void split3_cols_kernel(const float* __restric
   write_record(v, out + idx * kRec);
 }
 
-template <bool FX>
+template <bool FX, int NB = 4>
 __device__ __forceinline__ void wait_vmcnt_stage(bool more) {
   if (!more) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   else if (FX) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // kDmaFX: the next stage may fly
+  else if (NB == 1) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");  // 30 DMAs over 4 waves: 7 or 8 each
+  else if (NB == 2) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");  // 36 DMAs: 9 each
   else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");          // kDmaPerWave
 }
 static_assert(kDmaPerWave == 12 && kDmaFX == 10, "wait_vmcnt_stage assumes 12 / 10 DMA instructions per wave");
@@ -203,18 +205,34 @@ __device__ __forceinline__ void split8(const float (&v)[8], bf16x8& p0, bf16x8& 
 // 69-70 vs 58 ms at 8192 (profiles/r01c_dense_split3_tiles.txt): kept 256.
 // FX: B operand straight from fp32 X (split in registers) instead of the split
 // pass's XB records; X rows readable up to `pread` floats (>= P, % 4 == 0).
-template <int PROBE, bool FX>
+// NB: 32-column blocks per wave along P.  NB = 4 is the 256 x 256 tile; NB = 1
+// / 2 (256 x 64 / 256 x 128 tiles, quarters / halves of a 256 x 256 tile) run
+// the last, partial wave of tiles on four / two times as many CUs.  Every output
+// element sees the same k-steps and the same six MFMAs in the same order
+// under either width, so the two are bit-identical.
+template <int PROBE, bool FX, int NB = 4>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void dense_split3_kernel(const uint8_t* __restrict__ WA, const uint8_t* __restrict__ XB, float* __restrict__ Y,
                          int64_t ldy, int M, int64_t P, int64_t Mp, int64_t Pp, int n_stages, int n_mt,
                          int64_t n_pt, int64_t tiles_per_xcd, int group_m, const float* __restrict__ X,
-                         int64_t ldx, int K, int64_t pread) {
-  constexpr int kStage = FX ? kStageFX : kStageBytes;
-  constexpr int kDma = FX ? kDmaFX : kDmaPerWave;
+                         int64_t ldx, int K, int64_t pread, int64_t t_base, int64_t t_end) {
+  static_assert(NB == 4 || ((NB == 1 || NB == 2) && !FX && PROBE == 0), "narrow tiles: split-pass operands only");
+  constexpr int BN = 64 * NB;                              // tile width along P
+  constexpr int kStage = FX ? kStageFX : kOpStage + 2 * BN * kRec;
+  constexpr int kDmaTot = FX ? 4 * kDmaFX : 24 + 6 * NB;   // 1-KiB DMA pieces per stage
+  constexpr int kDma = (kDmaTot + 3) / 4;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const int64_t j = blockIdx.x >> 3;
-  const int64_t t = (blockIdx.x & 7) * tiles_per_xcd + j;
-  if (j >= tiles_per_xcd || t >= int64_t(n_mt) * n_pt) return;
+  int64_t t;
+  int quarter = 0;
+  if constexpr (NB == 4) {
+    const int64_t j = blockIdx.x >> 3;
+    t = (blockIdx.x & 7) * tiles_per_xcd + j;
+    if (j >= tiles_per_xcd || t >= t_end) return;
+  } else {
+    t = t_base + blockIdx.x / (4 / NB);
+    quarter = blockIdx.x % (4 / NB);
+    if (t >= t_end) return;
+  }
   const int64_t per_group = int64_t(group_m) * n_pt;
   const int g = int(t / per_group);
   const int first_m = g * group_m;
@@ -230,7 +248,8 @@ void dense_split3_kernel(const uint8_t* __restrict__ WA, const uint8_t* __restri
 
   // stage s holds k-groups 2s, 2s+1 of both operands: [A kg0 | A kg1 | B kg0 | B kg1], 12 KiB each
   const uint8_t* srcA = WA + int64_t(mt) * kTile * kRec + lane * 16;
-  const uint8_t* srcB = XB + pt * kTile * kRec + lane * 16;
+  const int64_t col0 = pt * kTile + quarter * BN;          // first P column of the tile
+  const uint8_t* srcB = XB + col0 * kRec + lane * 16;
   const int64_t pitchA = Mp * kRec, pitchB = Pp * kRec;  // bytes per k-group
   auto issue = [&](int s) {
     if constexpr (PROBE == 1 || PROBE == 3) return;
@@ -238,6 +257,13 @@ void dense_split3_kernel(const uint8_t* __restrict__ WA, const uint8_t* __restri
 #pragma unroll
     for (int i = 0; i < kDma; ++i) {
       const int q = wave + 4 * i;      // 1 KiB each (A records) / one fp32 row of 256 p (FX B)
+      if (kDmaTot % 4 && q >= kDmaTot) continue;
+      if (!FX && NB != 4 && q >= 24) {  // narrow B: 3 * NB pieces per k-group
+        const int qb = q - 24, kgl = qb / (3 * NB), chunk = qb % (3 * NB);
+        const uint8_t* src = srcB + (2 * int64_t(s) + kgl) * pitchB + chunk * 1024;
+        __builtin_amdgcn_global_load_lds(DOL_GPTR(src), DOL_LPTR(st + q * 1024), 16, 0, 0);
+        continue;
+      }
       if (FX && q >= 24) {
         const int k = min(16 * s + (q - 24), K - 1);     // rows past K: masked after the read
         int64_t c = pt * kTile + lane * 4;
@@ -253,15 +279,15 @@ void dense_split3_kernel(const uint8_t* __restrict__ WA, const uint8_t* __restri
     }
   };
 
-  f32x16 acc[4][4];
+  f32x16 acc[4][NB];
 #pragma unroll
   for (int a = 0; a < 4; ++a)
 #pragma unroll
-    for (int b = 0; b < 4; ++b)
+    for (int b = 0; b < NB; ++b)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
 
-  auto read_frags = [&](int s, bf16x8 (&fa)[4][3], bf16x8 (&fb)[4][3]) {
+  auto read_frags = [&](int s, bf16x8 (&fa)[4][3], bf16x8 (&fb)[NB][3]) {
     const uint8_t* st = lds + (s % kStages) * kStage;
     const uint8_t* sa = st + h * (kTile * kRec) + (wm * 128 + li) * kRec;
 #pragma unroll
@@ -285,20 +311,20 @@ void dense_split3_kernel(const uint8_t* __restrict__ WA, const uint8_t* __restri
         split8(v, fb[i][0], fb[i][1], fb[i][2]);
       }
     } else {
-      const uint8_t* sb = st + kOpStage + h * (kTile * kRec) + (wn * 128 + li) * kRec;
+      const uint8_t* sb = st + kOpStage + h * (BN * kRec) + (wn * 32 * NB + li) * kRec;
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < NB; ++i)
 #pragma unroll
         for (int p = 0; p < 3; ++p) fb[i][p] = *reinterpret_cast<const bf16x8*>(sb + i * 32 * kRec + 16 * p);
     }
   };
   // the six piece products of one 32x32x16 block, smallest first
-  auto mfmas = [&](const bf16x8 (&fa)[4][3], const bf16x8 (&fb)[4][3]) {
+  auto mfmas = [&](const bf16x8 (&fa)[4][3], const bf16x8 (&fb)[NB][3]) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
-      for (int b = 0; b < 4; ++b) {
+      for (int b = 0; b < NB; ++b) {
         f32x16 c = acc[a][b];
         c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a][2], fb[b][0], c, 0, 0, 0);
         c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a][0], fb[b][2], c, 0, 0, 0);
@@ -318,11 +344,11 @@ void dense_split3_kernel(const uint8_t* __restrict__ WA, const uint8_t* __restri
   issue(0);
   if (n_stages > 1) issue(1);
   for (int s = 0; s < n_stages; ++s) {
-    wait_vmcnt_stage<FX>(s + 1 < n_stages);  // my DMA of stage s landed
+    wait_vmcnt_stage<FX, NB>(s + 1 < n_stages);  // my DMA of stage s landed
     barrier();                           // ... and every wave's; stage (s + 2) % 3 is free
     if (s + 2 < n_stages) issue(s + 2);
     if constexpr (PROBE == 2) continue;
-    bf16x8 fa[4][3], fb[4][3];
+    bf16x8 fa[4][3], fb[NB][3];
     read_frags(s, fa, fb);
     mfmas(fa, fb);
   }
@@ -330,8 +356,8 @@ void dense_split3_kernel(const uint8_t* __restrict__ WA, const uint8_t* __restri
 #pragma unroll
   for (int a = 0; a < 4; ++a)
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const int64_t col = pt * kTile + wn * 128 + b * 32 + li;
+    for (int b = 0; b < NB; ++b) {
+      const int64_t col = col0 + wn * 32 * NB + b * 32 + li;
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int row = mt * kTile + wm * 128 + a * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
@@ -411,34 +437,59 @@ extern "C" int dol_mix_dense_split3_f32(const float* W, int64_t ldw, const float
     hipLaunchKernelGGL(split3_cols_kernel, dim3(static_cast<unsigned>(cdiv(n, 256))), dim3(256), 0, s, X, ldx, K, P,
                        g.Pp, static_cast<int>(g.Kg), xb);
   }
-  const int n_mt = static_cast<int>(g.Mp / kTile);
-  const int64_t n_pt = g.Pp / kTile;
-  const int64_t tiles_per_xcd = cdiv(int64_t(n_mt) * n_pt, 8);
-  if (8 * tiles_per_xcd >= (int64_t(1) << 32)) return fail(DOL_EINVAL, "dol_mix_dense_split3_f32: too many tiles");
   // diagnostics knobs (tools/gpu_dense_probe.sh); read once per process
   static const int probe = [] { const char* e = getenv("DOL_SPLIT3_PROBE"); return e ? atoi(e) : 0; }();
   static const int group_m = [] {
     const char* e = getenv("DOL_SPLIT3_GROUP_M");
     return e && atoi(e) > 0 ? atoi(e) : kGroupM;
   }();
+  const int n_mt = static_cast<int>(g.Mp / kTile);
+  const int64_t n_pt = g.Pp / kTile;
+  const int64_t n_tiles = int64_t(n_mt) * n_pt;
+  // Tail: when the last wave of 256 x 256 tiles would fill at most a quarter
+  // (a half) of the CUs, those tiles run as 256 x 64 quarters (256 x 128
+  // halves) in a second launch: 1024 agents x 101,770 = 1592 tiles = 6 x 256 +
+  // 56 -> quarters, 2048 agents = 12 x 256 + 112 -> halves.  DOL_SPLIT3_CUS overrides the
+  // CU count (tests force the tail path at small sizes; 0 disables it).
+  static const int n_cu = [] {
+    int dev = 0, cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cu = 0;
+    return cu;
+  }();
+  const char* cus_env = getenv("DOL_SPLIT3_CUS");
+  const int64_t cus = cus_env && *cus_env ? atoi(cus_env) : n_cu;
+  const int64_t tail = cus > 0 ? n_tiles % cus : 0;
+  const bool narrow_tail = !fx && probe == 0 && n_tiles > cus && tail > 0 && 2 * tail <= cus;
+  const int nb_tail = 4 * tail <= cus ? 1 : 2;
+  const int64_t t_main = narrow_tail ? n_tiles - tail : n_tiles;
+  const int64_t tiles_per_xcd = cdiv(t_main, 8);
+  if (8 * tiles_per_xcd >= (int64_t(1) << 32) || 4 * tail >= (int64_t(1) << 32))
+    return fail(DOL_EINVAL, "dol_mix_dense_split3_f32: too many tiles");
   const int64_t pread = (P % 4 == 0) ? P : (P + 3) / 4 * 4;
-  auto launch = [&](auto kern, int lds) {
+  auto launch = [&](auto kern, int lds, int64_t grid, int64_t t_base, int64_t t_end) {
     // > 64 KiB of dynamic LDS: set on every call (cheap), so every device of the process gets it
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(8 * tiles_per_xcd)), dim3(256), lds, s, wa, xb, Y, ldy, M,
+    hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(grid)), dim3(256), lds, s, wa, xb, Y, ldy, M,
                        P, g.Mp, g.Pp, static_cast<int>(g.Kg / 2), n_mt, n_pt, tiles_per_xcd, group_m, X, ldx, K,
-                       pread);
+                       pread, t_base, t_end);
   };
+  const int64_t grid = 8 * tiles_per_xcd;
   if (fx) {
-    if (probe == 1) launch(dense_split3_kernel<1, true>, kStages * kStageFX);
-    else if (probe == 2) launch(dense_split3_kernel<2, true>, kStages * kStageFX);
-    else launch(dense_split3_kernel<0, true>, kStages * kStageFX);
+    if (probe == 1) launch(dense_split3_kernel<1, true>, kStages * kStageFX, grid, 0, t_main);
+    else if (probe == 2) launch(dense_split3_kernel<2, true>, kStages * kStageFX, grid, 0, t_main);
+    else launch(dense_split3_kernel<0, true>, kStages * kStageFX, grid, 0, t_main);
   } else {
-    if (probe == 1) launch(dense_split3_kernel<1, false>, kLds);
-    else if (probe == 2) launch(dense_split3_kernel<2, false>, kLds);
-    else if (probe == 3) launch(dense_split3_kernel<3, false>, kLds);
-    else if (probe == 4) launch(dense_split3_kernel<4, false>, kLds);
-    else launch(dense_split3_kernel<0, false>, kLds);
+    if (probe == 1) launch(dense_split3_kernel<1, false>, kLds, grid, 0, t_main);
+    else if (probe == 2) launch(dense_split3_kernel<2, false>, kLds, grid, 0, t_main);
+    else if (probe == 3) launch(dense_split3_kernel<3, false>, kLds, grid, 0, t_main);
+    else if (probe == 4) launch(dense_split3_kernel<4, false>, kLds, grid, 0, t_main);
+    else launch(dense_split3_kernel<0, false>, kLds, grid, 0, t_main);
   }
+  if (narrow_tail && nb_tail == 1)
+    launch(dense_split3_kernel<0, false, 1>, kStages * (kOpStage + 2 * 64 * kRec), 4 * tail, t_main, n_tiles);
+  else if (narrow_tail)
+    launch(dense_split3_kernel<0, false, 2>, kStages * (kOpStage + 2 * 128 * kRec), 2 * tail, t_main, n_tiles);
   return dol::check_launch("dol_mix_dense_split3_f32");
 }

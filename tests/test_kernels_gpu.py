@@ -404,6 +404,36 @@ def test_mix_dense_split3_matches_f32_kernel_and_ragged_rows(gpu):
     assert e_split.max() <= 2 * e_f32.max() + 1e-30
 
 
+@pytest.mark.parametrize("M,K,P,cus", [(300, 300, 2148, 16), (256, 777, 5137, 20), (513, 64, 3001, 32),
+                                       (300, 300, 2148, 14), (513, 64, 3001, 10), (1024, 1024, 101770, None)])
+def test_mix_dense_split3_narrow_tail_bit_identical(M, K, P, cus, gpu, monkeypatch):
+    """The last partial wave of 256 x 256 tiles runs as 256 x 64 quarters
+    (dense_split3_kernel<.., NB = 1>) when it would fill <= 1/4 of the CUs, as
+    256 x 128 halves (NB = 2) when <= 1/2 (cus = 14, 10 here);
+    DOL_SPLIT3_CUS pretends a CU count so small shapes take that path (None:
+    the device's own, 1592 tiles at the bench shape = 6 x 256 + 56).  Same bits
+    as all-wide tiles (DOL_SPLIT3_CUS=0), incl. ragged rows / columns / K and
+    padding columns past P left untouched."""
+    rng = np.random.default_rng(M + K + P)
+    W = ((rng.random((M, K)) < 0.2) * rng.random((M, K))).astype(np.float32)
+    X = rng.standard_normal((K, P)).astype(np.float32)
+    Wd, Xd = dev(W, gpu), padded(X, gpu, 3)
+    Y1, Y2 = padded(np.zeros((M, P), np.float32), gpu, 3), padded(np.zeros((M, P), np.float32), gpu, 3)
+    if cus is None:
+        monkeypatch.delenv("DOL_SPLIT3_CUS", raising=False)
+    else:
+        monkeypatch.setenv("DOL_SPLIT3_CUS", str(cus))
+    ops.mix_dense_split3(Wd, Xd, Y1, P=P)
+    monkeypatch.setenv("DOL_SPLIT3_CUS", "0")
+    ops.mix_dense_split3(Wd, Xd, Y2, P=P)
+    torch.cuda.synchronize()
+    assert bits_equal(Y1[:, :P].cpu().numpy(), Y2[:, :P].cpu().numpy())
+    assert np.isnan(Y1[:, P:].cpu().numpy()).all()
+    if M * K * P <= 1 << 31:
+        want64 = W.astype(np.float64) @ X.astype(np.float64)
+        assert np.all(np.abs(Y1[:, :P].cpu().numpy() - want64) <= _split3_bound(W, X) + 1e-30)
+
+
 @pytest.mark.parametrize("M,K,P,extra", [(256, 256, 1024, 0), (130, 37, 1031, 1), (300, 600, 5000, 4),
                                          (64, 20, 4, 0), (513, 300, 701, 3), (200, 50, 999, 0)])
 def test_mix_dense_split3_fused_x_equals_split_pass(M, K, P, extra, gpu):
