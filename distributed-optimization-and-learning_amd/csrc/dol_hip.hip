@@ -250,12 +250,16 @@ __global__ __launch_bounds__(kThreads) void ring_mix_kernel(
 // must hit L2), waits on its own vmcnt, reads its lanes back and stores with
 // nontemporal stores.  No barrier: a wave only reads what it loaded.  On
 // MI355X (tools/membench7/8.hip, same box): 6.17 TB/s vs 5.91 for the
-// register-staged kernel, = the measured copy ceiling (6.16); nt loads here
-// cost 17 % (they evict the halo rows from L2).
+// register-staged kernel, = the measured copy ceiling (6.16); nt loads on
+// every row cost 17 % (they evict the halo rows from L2), but nt on the R - 2
+// rows no other tile reads (NTI, default; DOL_RING_NTI=0 turns it off) gains
+// 2.3 %: 10.90-10.93 vs 11.15-11.16 ms at 8192 x 2^20, three A/B pairs on
+// one box (profiles/r01d_ring_nti.txt).  The same split in ring_steps_kernel
+// gained nothing.
 #define DOL_GPTR(p) ((const __attribute__((address_space(1))) void*)(p))
 #define DOL_LPTR(p) ((__attribute__((address_space(3))) void*)(p))
 
-template <int R, class Epi = NoEpi>
+template <int R, class Epi = NoEpi, bool NTI = false>
 __global__ __launch_bounds__(kThreads) void ring_mix_dma_kernel(
     const float* __restrict__ X, int64_t ldx, float* __restrict__ Y, int64_t ldy, int n_rows,
     int64_t ncols_v, int64_t n_col_tiles, const float* __restrict__ halo_prev,
@@ -276,7 +280,10 @@ __global__ __launch_bounds__(kThreads) void ring_mix_dma_kernel(
 #pragma unroll
   for (int k = 0; k < R + 2; ++k) {
     const int r = min(r0 - 1 + k, r1);
-    __builtin_amdgcn_global_load_lds(DOL_GPTR(row(r) + 4 * c), DOL_LPTR(&lds[wave][k][0]), 16, 0, 0);
+    if (NTI && k >= 2 && k < R)  // rows no other tile reads: nontemporal
+      __builtin_amdgcn_global_load_lds(DOL_GPTR(row(r) + 4 * c), DOL_LPTR(&lds[wave][k][0]), 16, 0, 2);
+    else
+      __builtin_amdgcn_global_load_lds(DOL_GPTR(row(r) + 4 * c), DOL_LPTR(&lds[wave][k][0]), 16, 0, 0);
   }
   decltype(epi.template load<f4>(0, 0)) es[R];  // epilogue operands ride with the DMA
 #pragma unroll
@@ -987,6 +994,10 @@ int mix_ring_impl(const char* nm, const float* X, int64_t ldx, float* Y, int64_t
     if (dma) {
       constexpr int R = 4;
       if (nct * cdiv(n_rows, R) > kMaxBlocks) return fail(DOL_EINVAL, "%s: problem too large for one launch", nm);
+      if (env_int("DOL_RING_NTI", 1))
+        hipLaunchKernelGGL((ring_mix_dma_kernel<R, Epi, true>), dim3(static_cast<unsigned>(nct * cdiv(n_rows, R))),
+                           dim3(kThreads), 0, s, X, ldx, Y, ldy, n_rows, cs.n4, nct, halo_prev, halo_next, w_prev, w_next, epi);
+      else
       hipLaunchKernelGGL((ring_mix_dma_kernel<R, Epi>), dim3(static_cast<unsigned>(nct * cdiv(n_rows, R))), dim3(kThreads),
                          0, s, X, ldx, Y, ldy, n_rows, cs.n4, nct, halo_prev, halo_next, w_prev, w_next, epi);
     } else if constexpr (kPlain) {
