@@ -66,7 +66,7 @@ def ring_weights(n: int):
     return rw
 
 
-def copy_peak(device, gib: float = 2.0, reps: int = 10) -> float:
+def copy_peak(device, gib: float = 8.0, reps: int = 20) -> float:
     from dolhip import ops
     n = int(gib * (1 << 30) / 4)
     a = torch.empty(n, dtype=torch.float32, device=device).normal_()
