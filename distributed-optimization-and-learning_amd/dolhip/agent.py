@@ -79,7 +79,9 @@ class BankSGD:
     """torch.optim.SGD(lr, momentum) over one bank row, as ONE fused HIP kernel
     (dol_prox_admm_sgd_f32 with theta = NULL): buf = g (first step) or
     buf*mu + g; w = fma(-lr, buf, w).  Momentum persists across rounds, as the
-    reference's optimizer state does (it is never reset)."""
+    reference's optimizer state does (it is never reset).  Whether a row's
+    buffer has started lives in the bank (`AgentBank.mom_started`), so it
+    moves with `attach` and survives `AgentBank.save/load`."""
 
     def __init__(self, agent: "BankAgent", lr: float, momentum: float = 0.0):
         self.agent = agent
@@ -98,8 +100,10 @@ class BankSGD:
         ops.prox_admm_sgd(b.buffer("x")[i:i + 1], b.buffer("grad")[i:i + 1],
                           buf=b.buffer("mom")[i:i + 1] if self.momentum != 0.0 else None,
                           theta=theta, alpha=b.buffer("alpha", zero=True)[i:i + 1] if alpha else None,
-                          rho=rho, lr=self.lr, momentum=self.momentum, first_step=self.steps == 0,
+                          rho=rho, lr=self.lr, momentum=self.momentum, first_step=not b.mom_started[i],
                           write_grad=True, P=b.P)
+        if self.momentum != 0.0:
+            b.mom_started[i] = True
         self.steps += 1
 
 
@@ -122,6 +126,7 @@ class BankAgent:
         for name in ("x", "grad", "mom", "alpha"):
             if old.has(name):
                 bank.buffer(name, zero=True)[row, : bank.P].copy_(old.buffer(name)[oi, : old.P])
+        bank.mom_started[row] = old.mom_started[oi]
         self.bank, self.row = bank, row
         bank.buffer("grad", zero=True)
         bank.bind(row, self.model)

@@ -71,6 +71,10 @@ class AgentBank:
         self.ld = int(ld) if ld is not None else row_stride(self.P)
         self._buf: Dict[str, torch.Tensor] = {}
         self._modules: List[Optional[torch.nn.Module]] = [None] * self.n
+        # per row: has the SGD momentum buffer been written yet?  torch.optim.SGD
+        # takes buf = g on a parameter's first step and buf*mu + g after; the
+        # flag is saved with the checkpoint so a resumed run keeps its momentum.
+        self.mom_started: List[bool] = [False] * self.n
         self.offsets = []
         off = 0
         for k, shape in self.layout:
@@ -194,7 +198,8 @@ class AgentBank:
         (no pickles).  The reference keeps no model checkpoints."""
         from safetensors.torch import save_file
         tensors = {n: self.rows(n).contiguous().cpu() for n in names if self.has(n)}
-        meta = {"P": str(self.P), "n": str(self.n), "layout": repr(self.layout)}
+        meta = {"P": str(self.P), "n": str(self.n), "layout": repr(self.layout),
+                "mom_started": "".join("1" if f else "0" for f in self.mom_started)}
         save_file(tensors, path, metadata=meta)
 
     def load(self, path: str) -> None:
@@ -205,6 +210,11 @@ class AgentBank:
                 raise ValueError(f"checkpoint is [{meta.get('n')}, {meta.get('P')}], bank is [{self.n}, {self.P}]")
             for name in f.keys():
                 self.buffer(name, zero=True)[:, : self.P].copy_(f.get_tensor(name))
+            flags = meta.get("mom_started")
+            if flags is not None and len(flags) == self.n:
+                self.mom_started = [c == "1" for c in flags]
+            elif "mom" in f.keys():  # older checkpoint: a saved momentum buffer is a started one
+                self.mom_started = [True] * self.n
         self.rebind_all()
 
     def unflatten(self, vec: torch.Tensor) -> Dict[str, torch.Tensor]:

@@ -81,31 +81,55 @@ def synthetic_pair(name: str, n_train: int = 6000, n_test: int = 1000, seed: int
     return (SyntheticImages(n_train, shape, 10, seed), SyntheticImages(n_test, shape, 10, seed + 1))
 
 
-def torchvision_pair(name: str, root: str):
+def dataset_spec(name: str, project: str):
+    """(torchvision class name, data_dir, Normalize mean, Normalize std) exactly
+    as each project's get_dataset picks them.
+
+    * project "dist" (DIST/utils.py:72-95): dir ``../data/<name>/``; cifar10 /
+      cifar100 (0.5,)*3; mnist (0.1307,)/(0.3081,); fmnist (0.5,)*3 — three
+      channels on a 1-channel image, which torchvision's in-place Normalize
+      rejects at the first item, as in the reference.  Any other name leaves
+      the reference's train_dataset unbound (UnboundLocalError); here a
+      ValueError.
+    * project "dec" (DEC/utils.py:97-137): cifar10 in ``../data/cifar/``;
+      every other name takes the mnist/fmnist branch (``args.dataset ==
+      'mnist' or 'fmnist'`` is always true): mnist in ``../data/mnist/``,
+      anything else FashionMNIST in ``../data/fmnist/`` — both with the MNIST
+      statistics (0.1307,)/(0.3081,).
+    """
+    half3, mnist = ((0.5, 0.5, 0.5), (0.5, 0.5, 0.5)), ((0.1307,), (0.3081,))
+    if project == "dist":
+        table = {"cifar10": ("CIFAR10",) + half3, "cifar100": ("CIFAR100",) + half3,
+                 "mnist": ("MNIST",) + mnist, "fmnist": ("FashionMNIST",) + half3}
+        if name not in table:
+            raise ValueError(f"unknown dataset '{name}' (DIST/utils.py:76-95 knows {sorted(table)})")
+        cls, mean, std = table[name]
+        return cls, f"../data/{name}/", mean, std
+    if project == "dec":
+        if name == "cifar10":
+            return ("CIFAR10", "../data/cifar/") + half3
+        if name == "mnist":
+            return ("MNIST", "../data/mnist/") + mnist
+        return ("FashionMNIST", "../data/fmnist/") + mnist
+    raise ValueError(f"project must be 'dist' or 'dec', not {project!r}")
+
+
+def torchvision_pair(name: str, project: str):
+    cls, root, mean, std = dataset_spec(name, project)
     try:
-        from torchvision import datasets, transforms  # noqa: F401
+        from torchvision import datasets, transforms
     except ImportError as e:  # no torchvision in this image: say what to use instead
         raise ImportError(f"dataset '{name}' needs torchvision (not installed); use dataset='synthetic'") from e
-    if name == "cifar10":
-        tf = transforms.Compose([transforms.ToTensor(), transforms.Normalize((0.5,) * 3, (0.5,) * 3)])
-        return (datasets.CIFAR10(root, train=True, download=True, transform=tf),
-                datasets.CIFAR10(root, train=False, download=True, transform=tf))
-    if name == "cifar100":
-        tf = transforms.Compose([transforms.ToTensor(), transforms.Normalize((0.5,) * 3, (0.5,) * 3)])
-        return (datasets.CIFAR100(root, train=True, download=True, transform=tf),
-                datasets.CIFAR100(root, train=False, download=True, transform=tf))
-    if name == "fmnist":
-        tf = transforms.Compose([transforms.ToTensor(), transforms.Normalize((0.5,), (0.5,))])
-        return (datasets.FashionMNIST(root, train=True, download=True, transform=tf),
-                datasets.FashionMNIST(root, train=False, download=True, transform=tf))
-    tf = transforms.Compose([transforms.ToTensor(), transforms.Normalize((0.1307,), (0.3081,))])
-    return (datasets.MNIST(root, train=True, download=True, transform=tf),
-            datasets.MNIST(root, train=False, download=True, transform=tf))
+    tf = transforms.Compose([transforms.ToTensor(), transforms.Normalize(mean, std)])
+    ctor = getattr(datasets, cls)
+    return (ctor(root, train=True, download=True, transform=tf), ctor(root, train=False, download=True, transform=tf))
 
 
-def load_pair(args):
+def load_pair(args, project: str):
+    """(train, test) for one project ('dist' = weighted_average, 'dec' =
+    primal_dual); 'synthetic*' names work offline."""
     name = args.dataset or "mnist"
     if str(name).startswith("synthetic"):
         return synthetic_pair(name, args.synthetic_train or 6000, args.synthetic_test or 1000,
                               args.synthetic_seed if args.synthetic_seed is not None else 1234)
-    return torchvision_pair(name, f"../data/{name}/")
+    return torchvision_pair(name, project)

@@ -187,6 +187,25 @@ class CSR:
     def nnz(self) -> int:
         return int(self.col.size)
 
+    def validate(self) -> "CSR":
+        """Raise ValueError unless the arrays form a well-formed CSR: rowptr has
+        n_rows + 1 entries, starts at 0, never decreases and ends at nnz; every
+        column index is in [0, n_cols); one value per entry.  MixingPlan runs
+        this once per graph; the raw ops (ops.mix_csr, dol_mix_csr_f32) trust
+        their inputs and would read out of bounds on a malformed CSR."""
+        rp, col = np.asarray(self.rowptr), np.asarray(self.col)
+        if rp.ndim != 1 or rp.size != self.n_rows + 1:
+            raise ValueError(f"rowptr has {rp.size} entries, expected n_rows + 1 = {self.n_rows + 1}")
+        if rp[0] != 0 or rp[-1] != col.size:
+            raise ValueError(f"rowptr must start at 0 and end at nnz = {col.size} (got {rp[0]} .. {rp[-1]})")
+        if np.any(np.diff(rp.astype(np.int64)) < 0):
+            raise ValueError("rowptr decreases")
+        if np.asarray(self.val).size != col.size:
+            raise ValueError("col and val lengths differ")
+        if col.size and (col.min() < 0 or col.max() >= self.n_cols):
+            raise ValueError(f"column index out of [0, {self.n_cols})")
+        return self
+
     def ring_weights(self):
         """(w_prev, w_next) if every row i is exactly {i-1, i+1} (mod n), n >= 3."""
         n = self.n_rows
@@ -331,7 +350,7 @@ class MixingPlan:
             raise ValueError(f"dense_kernel must be one of {self.DENSE_KERNELS}")
         self.dense_kernel = dense_kernel
         self._work, self._work_key = None, None
-        self.csr = csr
+        self.csr = csr.validate()
         self.device = torch.device(device)
         self.n_rows = csr.n_rows
         self.rowptr = torch.from_numpy(csr.rowptr).to(self.device)
@@ -397,6 +416,7 @@ class MixingPlan:
         layout allow (ring, P % 4 == 0, 16-B aligned rows); returns how many
         rounds were applied (>= 1).  Bit-identical to single rounds."""
         P = X.shape[1] if P is None else P
+        self._check_x(X)
         k = min(int(steps), self.MAX_FUSED_STEPS)
         if (k > 1 and self.kind == "ring" and P % 4 == 0 and X.data_ptr() % 16 == 0 and Y.data_ptr() % 16 == 0
                 and X.stride(0) % 4 == 0 and Y.stride(0) % 4 == 0):
@@ -406,8 +426,14 @@ class MixingPlan:
         self.apply(X, Y, P=P)
         return 1
 
+    def _check_x(self, X: torch.Tensor) -> None:
+        need = self.csr.n_cols if self.csr is not None else self.W.shape[1]
+        if X.shape[0] < need:
+            raise ValueError(f"X has {X.shape[0]} rows; W has {need} columns")
+
     def apply(self, X: torch.Tensor, Y: torch.Tensor, P: Optional[int] = None) -> torch.Tensor:
         from . import ops
+        self._check_x(X)
         if self.kind == "ring":
             return ops.mix_ring(X, Y, self.w_prev, self.w_next, P=P, n_rows=self.n_rows)
         if self.kind == "dense":
@@ -420,6 +446,7 @@ class MixingPlan:
                   first_step: bool = False, P: Optional[int] = None) -> torch.Tensor:
         """One fused DGD round (mix + local steps, BASELINE config 3); ring or CSR."""
         from . import ops
+        self._check_x(X)
         kw = dict(mom=mom, objective=objective, steps=steps, lr=lr, momentum=momentum, first_step=first_step, P=P)
         if self.kind == "ring":
             return ops.dgd_ring(X, Y, self.w_prev, self.w_next, target, n_rows=self.n_rows, **kw)

@@ -284,7 +284,7 @@ def global_mean_exact(local_rows: torch.Tensor, lo: int, hi: int, order: Sequenc
     for k, (o, ids) in enumerate(runs):
         if o == rank:
             if k > 0 and runs[k - 1][0] != rank:
-                dist.recv(acc[:P], src=runs[k - 1][0], group=group)
+                _p2p(dist.recv, acc[:P], runs[k - 1][0], group)
                 have = True
             idx = torch.as_tensor([g - lo for g in ids], dtype=torch.int32, device=device)
             last = k == len(runs) - 1
@@ -292,15 +292,34 @@ def global_mean_exact(local_rows: torch.Tensor, lo: int, hi: int, order: Sequenc
                             scale=float(m) if last else 1.0, P=P)
             have = True
             if not last and runs[k + 1][0] != rank:
-                dist.send(acc[:P], dst=runs[k + 1][0], group=group)
+                _p2p(dist.send, acc[:P], runs[k + 1][0], group)
     if world > 1:
-        dist.broadcast(acc[:P], src=runs[-1][0], group=group)
+        _p2p(dist.broadcast, acc[:P], runs[-1][0], group)
     return acc
+
+
+def _gloo_staged(t: torch.Tensor, group) -> bool:
+    """gloo reads raw host pointers: device tensors go through host memory."""
+    return t.device.type == "cuda" and dist.get_backend(group) == "gloo"
+
+
+def _p2p(fn, t: torch.Tensor, peer: int, group) -> None:
+    """dist.send / dist.recv / dist.broadcast of `t` with `peer` (dst / src),
+    staged through a host copy under gloo."""
+    if not _gloo_staged(t, group):
+        fn(t, peer, group=group)
+        return
+    host = t.cpu()
+    fn(host, peer, group=group)
+    if fn is not dist.send:
+        t.copy_(host)
 
 
 def _all_bounds(lo: int, hi: int, device, group=None) -> List[Tuple[int, int]]:
     world = dist.get_world_size(group)
-    mine = torch.tensor([lo, hi], dtype=torch.int64, device=device)
+    mine = torch.tensor([lo, hi], dtype=torch.int64)  # host: tiny, and valid for gloo and RCCL via .to()
+    if not (torch.device(device).type == "cuda" and dist.get_backend(group) == "gloo"):
+        mine = mine.to(device)
     allb = [torch.empty_like(mine) for _ in range(world)]
     dist.all_gather(allb, mine, group=group)
     return [(int(t[0]), int(t[1])) for t in allb]

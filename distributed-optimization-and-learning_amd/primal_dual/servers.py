@@ -137,6 +137,48 @@ class Server(object):
         with torch.no_grad():
             g.bank.flatten(theta, out=g.flat_params())
 
+    def plot(self):
+        """Per-client local-epoch curves (DEC/servers.py:95-120): an s x s block of
+        clients (s = ceil(sqrt(n))), each with a loss panel (train / val) and,
+        one grid row below it, an accuracy panel (train / val), from the
+        client's `history` rows that `update_weights` appends.  The reference
+        offsets the accuracy row by a literal 10 (= s at its n = 100) and runs
+        past the last client for non-square n (IndexError); here the offset is
+        s and the cells after the last client stay empty.  Clients never
+        sampled have no history and get empty panels, as the reference's
+        `except: pass` gives."""
+        import math
+
+        import matplotlib.pyplot as plt
+        import pandas as pd
+
+        n = self.args.num_users
+        s = math.ceil(math.sqrt(n))
+        fig, axs = plt.subplots(2 * s, s, figsize=(s * 2, s * 4), sharex=True, sharey="row", squeeze=False)
+        axs = axs.flat
+        for block in range(s):
+            for j in range(s):
+                c = block * s + j
+                if c >= n:
+                    break
+                loss_ax, acc_ax = axs[2 * block * s + j], axs[(2 * block + 1) * s + j]
+                hist = pd.DataFrame(self.clients[c].history)
+                loss_ax.set_title("Client #%d" % (c + 1))
+                loss_ax.set(xlabel="rounds", ylabel="loss")
+                acc_ax.set(xlabel="rounds", ylabel="accuracy")
+                loss_ax.label_outer()
+                acc_ax.label_outer()
+                if {"train_loss", "val_loss"} <= set(hist.columns):
+                    loss_ax.plot(hist["train_loss"], "b", label="train")
+                    loss_ax.plot(hist["val_loss"], "r", label="val")
+                    loss_ax.legend()
+                if {"train_acc", "val_acc"} <= set(hist.columns):
+                    acc_ax.plot(hist["train_acc"], "k", label="train")
+                    acc_ax.plot(hist["val_acc"], "g", label="val")
+                    acc_ax.legend()
+        plt.show()
+        return fig
+
 
 class FedAdmm_Server(Server):
     """Averages the plain local weights, as the reference (DEC/servers.py:121-127)."""

@@ -202,16 +202,24 @@ class FedLCon(Simulator):
 
     By default the eps mixing steps all take effect (X <- W^eps X) and args are
     used as given — the behaviour the notebook's saved output shows
-    (WA.ipynb cell[36]).  args.reference_compat=True reproduces the shipped
-    code instead: __init__ forces num_users=1, local_ep=1, iid=True, and only
-    the first of the eps steps takes effect (new_weights is never reset)."""
+    (WA.ipynb cell[36]); this is a deliberate deviation from the shipped loop,
+    whose eps > 1 semantics no reference output pins (parity unpinned).  Two
+    flags reproduce the shipped code's quirks separately:
+      * args.reference_args_override — __init__ forces num_users=1,
+        local_ep=1, iid=True (DIST/simulators.py:177-180);
+      * args.reference_first_step_only — only the first of the eps steps
+        takes effect, since new_weights is never reset (:189-196).
+    args.reference_compat=True turns both on."""
 
     def __init__(self, args):
-        if args.reference_compat:
+        if args.reference_compat or args.reference_args_override:
             args.num_users = 1
             args.local_ep = 1
             args.iid = True
         super().__init__(args)
+
+    def _first_step_only(self) -> bool:
+        return bool(self.args.reference_compat or self.args.reference_first_step_only)
 
     def run(self, rounds, eps):
         start_time = time.time()
@@ -222,7 +230,7 @@ class FedLCon(Simulator):
             for j in range(eps):
                 print(f"\n| Consesnsus Round {j} |")
             if eps > 0:
-                self.mix(t, steps=1 if self.args.reference_compat else eps)
+                self.mix(t, steps=1 if self._first_step_only() else eps)
             self._eval_after_mix(test_acc_1, test_loss_1, label="Consensus")
             self._local_updates(local_losses)
             self.report(local_losses, test_loss_1, test_acc_1)

@@ -101,9 +101,19 @@ def test_consensus_and_neighbors_bit_exact(gpu):
     assert oracle.bits_equal(_flat(sim.clients[3].model), want[3])
 
 
-@pytest.mark.parametrize("compat", [False, True])
+@pytest.mark.parametrize("compat", [False, True, "first_step_only"])
 def test_fedlcon_eps_steps(compat, gpu):
     m = load_project("weighted_average", ["simulators", "utils"])
+    if compat == "first_step_only":
+        # the shipped loop's single effective step, with several users kept
+        args = _small_dist_args(m["utils"], reference_first_step_only=True, num_users=5, local_ep=0)
+        sim = m["simulators"].FedLCon(args)
+        assert args.num_users == 5 and sim._first_step_only()
+        X = sim.bank.rows().cpu().numpy().copy()
+        c = sim.plan(0).csr
+        sim.run(1, 3)
+        assert oracle.bits_equal(sim.bank.rows().cpu().numpy(), oracle.mix_csr(X, c.rowptr, c.col, c.val))
+        return
     args = _small_dist_args(m["utils"], reference_compat=compat, num_users=5)
     sim = m["simulators"].FedLCon(args)
     if compat:
@@ -228,3 +238,65 @@ def test_gossip_variant_trajectories_match_reference(key, gpu):
     assert len(sim.clients) == len(ref["agents"])
     for c, r in zip(sim.clients, ref["agents"]):
         _check_summary(_flat(c.model), r, TRAJ["stride"])
+
+
+def test_notebook_plots_after_one_round(gpu):
+    """The notebooks' plotting calls on real 1-round runs (WA.ipynb cell[39-43],
+    PD.ipynb cells 15/20/25/27), matplotlib Agg backend."""
+    import matplotlib
+    matplotlib.use("Agg")
+    import matplotlib.pyplot as plt
+    m = load_project("weighted_average", ["simulators", "utils"])
+    sims = []
+    for cls in ("DecFedAvg", "NoConsDecFedAvg"):
+        sim = getattr(m["simulators"], cls)(_small_dist_args(m["utils"]))
+        sim.run(1)
+        sims.append(sim)
+    fig = m["utils"].servers_plot(sims, 5, 8, True, ["dec", "no_cons"])
+    assert [len(a.lines) for a in fig.axes] == [0, 2, 2, 2]
+    m = load_project("primal_dual", ["servers", "utils"])
+    servers = []
+    for cls in ("FedAvg_Server", "FedAdmm_Server"):
+        args = m["utils"].DotDict(dict(TRAJ["dec_args"], device="cuda"))
+        s = getattr(m["servers"], cls)(args)
+        s.run(TRAJ["frac"], 1)
+        f = s.plot()
+        assert sum(len(a.lines) for a in f.axes) == 4 * int(TRAJ["frac"] * args.num_users)
+        servers.append(s)
+    fig = m["utils"].servers_plot(servers, args.num_users, TRAJ["frac"], args.iid)
+    assert [ln.get_label() for ln in fig.axes[0].lines] == ["FedAvg", "FedAdmm"]
+    plt.close("all")
+
+
+def test_momentum_survives_checkpoint_resume(gpu, tmp_path):
+    """A resumed agent continues buf = mu*buf + g (it does not restart with
+    buf = g): two steps, save, load into a fresh bank, third step — equal to
+    three uninterrupted steps."""
+    from dolhip.agent import BankAgent, BankSGD
+
+    class A(BankAgent):
+        def __init__(self):
+            torch.manual_seed(3)
+            self._init_bank(torch.nn.Linear(5, 4), gpu)
+            self.optimizer = BankSGD(self, lr=0.1, momentum=0.5)
+
+    def grad_step(a, k):
+        a.zero_grad()
+        g = torch.Generator().manual_seed(k)
+        a.bank.buffer("grad")[0, : a.bank.P] = torch.randn(a.bank.P, generator=g).to(gpu)
+        a.optimizer.step()
+
+    ref = A()
+    for k in range(3):
+        grad_step(ref, k)
+    a = A()
+    for k in range(2):
+        grad_step(a, k)
+    p = str(tmp_path / "a.safetensors")
+    a.bank.save(p)
+    b = A()
+    b.bank.load(p)
+    assert b.bank.mom_started == [True]
+    grad_step(b, 2)
+    assert torch.equal(b.bank.rows(), ref.bank.rows())
+    assert torch.equal(b.bank.rows("mom"), ref.bank.rows("mom"))

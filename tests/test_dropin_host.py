@@ -15,7 +15,7 @@ def test_weighted_average_surface():
         assert hasattr(m["simulators"].Simulator, meth)
     for meth in ("local_update", "consensus", "inference", "train_val_test", "report"):
         assert hasattr(m["clients"].Client, meth)
-    for f in ("DotDict", "setup_seed", "DatasetSplit", "get_dataset", "exp_details"):
+    for f in ("DotDict", "setup_seed", "DatasetSplit", "get_dataset", "exp_details", "servers_plot"):
         assert hasattr(m["utils"], f)
 
 
@@ -23,8 +23,11 @@ def test_primal_dual_surface():
     m = load_project("primal_dual", ["servers", "clients", "utils", "models", "sampling"])
     for name in ("Server", "FedAvg_Server", "FedProx_Server", "FedAdmm_Server"):
         assert hasattr(m["servers"], name)
-    for meth in ("average_weights", "run", "avg_trainig_calculator", "update_global_model", "tarining"):
+    for meth in ("average_weights", "run", "avg_trainig_calculator", "update_global_model", "tarining", "plot"):
         assert hasattr(m["servers"].FedAdmm_Server, meth)
+    m2 = load_project("primal_dual", ["utils"])
+    for f in ("DotDict", "setup_seed", "DatasetSplit", "get_dataset", "exp_details", "servers_plot"):
+        assert hasattr(m2["utils"], f)
     for name in ("Client", "FedAvg_Client", "FedProx_Client", "FedAdmm_Client"):
         assert hasattr(m["clients"], name)
     for meth in ("update_weights", "update_model", "update_duals", "inference", "train_val_test"):

@@ -150,3 +150,23 @@ def test_dynamic_8192_is_sparse_and_fast():
     gs = G.communication_csr("dynamic", "stochastic", 8192)
     assert len(gs) == 8192 and all(g.nnz == 2 for g in gs[:10])
     assert time.time() - t < 60
+
+
+def test_csr_validate_rejects_malformed():
+    """A malformed CSR is an error when a MixingPlan is built, not an
+    out-of-bounds device read (advisor finding)."""
+    from dolhip.graph import CSR
+    ok = CSR(3, 3, np.array([0, 1, 3, 3], np.int32), np.array([1, 0, 2], np.int32), np.ones(3, np.float32))
+    assert ok.validate() is ok
+    bad = [
+        CSR(3, 3, np.array([0, 1, 3], np.int32), np.array([1, 0, 2], np.int32), np.ones(3, np.float32)),
+        CSR(3, 3, np.array([1, 1, 3, 3], np.int32), np.array([1, 0, 2], np.int32), np.ones(3, np.float32)),
+        CSR(3, 3, np.array([0, 2, 1, 3], np.int32), np.array([1, 0, 2], np.int32), np.ones(3, np.float32)),
+        CSR(3, 3, np.array([0, 1, 3, 4], np.int32), np.array([1, 0, 2], np.int32), np.ones(3, np.float32)),
+        CSR(3, 3, np.array([0, 1, 3, 3], np.int32), np.array([1, 0, 3], np.int32), np.ones(3, np.float32)),
+        CSR(3, 3, np.array([0, 1, 3, 3], np.int32), np.array([1, -1, 2], np.int32), np.ones(3, np.float32)),
+        CSR(3, 3, np.array([0, 1, 3, 3], np.int32), np.array([1, 0, 2], np.int32), np.ones(2, np.float32)),
+    ]
+    for c in bad:
+        with pytest.raises(ValueError):
+            c.validate()
