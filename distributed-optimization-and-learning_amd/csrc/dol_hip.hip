@@ -491,6 +491,135 @@ __global__ __launch_bounds__(kThreads) void csr_xcd_kernel(
 }
 
 // ----------------------------------------------------------------------------
+// LDS-slab CSR mix (graphs of up to 8192 agents, any W): the whole column slab
+// X[0..x_rows)[16L bytes] lives in the CU's LDS (128 KiB), so every X byte is
+// read from memory ONCE per round however many rows gather it, and the deg
+// gathers per output row are LDS reads.  One persistent 1024-thread workgroup
+// per CU walks slabs; each thread owns PER = 8 lane-rows (row = k * 1024/L +
+// tid / L, 16-B piece tid % L) for the image fill AND for the output, and
+// keeps those rows' first DMAX neighbour indices / weights in registers for
+// the whole kernel (the index chain is paid once, not per tile).  The next
+// slab's X pieces are loaded into registers while the current slab's rows are
+// summed (register-staged double buffering; the image itself is single).
+// Slab order is XCD-aware: at step t, workgroup w of XCD x (= blockIdx % 8,
+// a speed assumption only) takes slab (t*8 + x)*nw + w: the workgroups of one
+// XCD hold adjacent slabs at the same moment, so the narrow row pieces they
+// read (16 B at 8192 agents) share L2 lines and DRAM pages.  Sums: +0 start, ascending CSR order, no
+// FMA — the same arithmetic as csr_mix_kernel (bit-identical).  Rows whose
+// degree exceeds DMAX read their extra (col, val) entries from memory.
+// ----------------------------------------------------------------------------
+constexpr int kLdsSlabBytes = 128 * 1024;
+constexpr int kLdsT = 1024;  // threads per LDS-slab workgroup
+
+template <int L, int T, bool NT_STORE, class Epi = NoEpi>
+__global__ __launch_bounds__(T) void csr_lds_kernel(
+    const float* __restrict__ X, int64_t ldx, int x_rows, float* __restrict__ Y, int64_t ldy, int n_rows,
+    int64_t n_slabs, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
+    const float* __restrict__ val, Epi epi) {
+  constexpr int ROWS = kLdsSlabBytes / (16 * L);  // rows the image holds (8192 / L)
+  constexpr int RSTEP = T / L;                    // rows per lane-row step
+  constexpr int PER = ROWS / RSTEP;               // lane-rows per thread (8192 / T)
+  constexpr int DMAX = 4;                         // neighbours held in registers per row
+  static_assert(PER <= 32, "long-row flags must fit 32 bits");
+  // image rows [0, ROWS) + one zero row at ROWS: register slots past a row's
+  // degree point there with weight +0, and acc + (+0 * +0) == acc for every
+  // acc this sum can hold (it starts at +0 and so is never -0), so short
+  // rows need no per-entry branch
+  extern __shared__ __attribute__((aligned(16))) f4 img[];
+  const int tid = threadIdx.x;
+  const int piece = tid % L, rsub = tid / L;
+  if (tid < L) img[ROWS * L + tid] = f4{0.f, 0.f, 0.f, 0.f};
+
+  uint32_t cc[PER][DMAX / 2];  // columns, two 16-bit indices per register
+  float ww[PER][DMAX];
+  uint32_t longm = 0;          // bit k: lane-row k has more than DMAX neighbours
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int r = k * RSTEP + rsub;
+    const int rc = r < n_rows ? r : 0;
+    const int e0 = rowptr[rc];
+    const int dg = r < n_rows ? rowptr[rc + 1] - e0 : 0;
+    longm |= uint32_t(dg > DMAX) << k;
+#pragma unroll
+    for (int q = 0; q < DMAX; ++q) {
+      const bool in = q < dg;
+      const int e = in ? e0 + q : 0;
+      const uint32_t cq = in ? static_cast<uint32_t>(col[e]) : uint32_t(ROWS);
+      if (q % 2 == 0) cc[k][q / 2] = cq;
+      else cc[k][q / 2] |= cq << 16;
+      ww[k][q] = in ? val[e] : 0.0f;
+    }
+    __builtin_amdgcn_sched_barrier(0);  // bound the prologue's live addresses
+  }
+
+  const uint32_t xcd = blockIdx.x & 7u, wl = blockIdx.x >> 3, nw = gridDim.x >> 3;
+  auto slab = [&](int64_t t) -> int64_t { return (t * 8 + xcd) * nw + wl; };
+  // addresses = wave-uniform 64-bit row base (SGPRs) + a 32-bit lane offset
+  // (lane's row within the wave * ld + piece; the host checks 64 * ld * 4 <
+  // 2^32), so no per-row 64-bit VGPR addresses stay live across the loop
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63;
+  const int wrow = wave * (64 / L);  // the wave's first row within a step
+  const uint32_t xoff = static_cast<uint32_t>(((lane / L) * ldx + piece * 4) * 4);
+  const uint32_t yoff = static_cast<uint32_t>(((lane / L) * ldy + piece * 4) * 4);
+  f4 pf[PER];
+  // Every lane loads: a lane whose row is past x_rows re-reads its wave's
+  // first row (valid whenever the wave loads at all) into an image slot no
+  // column refers to, so the loads carry no per-lane branch.
+  auto fetch = [&](int64_t s) {
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      if (k * RSTEP + wrow < x_rows) {  // wave-uniform
+        const char* wb = reinterpret_cast<const char*>(X + (int64_t(k * RSTEP + wrow) * ldx + s * L * 4));
+        const uint32_t o = k * RSTEP + rsub < x_rows ? xoff : static_cast<uint32_t>(piece * 16);
+        pf[k] = *reinterpret_cast<const f4*>(wb + o);
+      }
+    }
+  };
+  if (slab(0) < n_slabs) fetch(slab(0));
+  for (int64_t t = 0;; ++t) {
+    const int64_t s = slab(t);
+    if (s >= n_slabs) break;
+#pragma unroll
+    for (int k = 0; k < PER; ++k)
+      if (k * RSTEP + wrow < x_rows) img[(k * RSTEP + rsub) * L + piece] = pf[k];
+    if (slab(t + 1) < n_slabs) fetch(slab(t + 1));
+    __syncthreads();
+    const int64_t cf = (s * L + piece) * 4;  // absolute float column of this lane's piece
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int r = k * RSTEP + rsub;
+      if (r < n_rows) {
+        // re-derive the LDS addresses each slab (an empty asm hides that they
+        // are loop-invariant: hoisted, they would cost PER * DMAX registers)
+        // (and the weights: the packed multiply wants each one duplicated
+        // into a register pair, which hoisted would double their footprint)
+        uint32_t c01 = cc[k][0], c23 = cc[k][1];
+        float w0 = ww[k][0], w1 = ww[k][1], w2 = ww[k][2], w3 = ww[k][3];
+        asm volatile("" : "+v"(c01), "+v"(c23), "+v"(w0), "+v"(w1), "+v"(w2), "+v"(w3));
+        const auto es = epi.template load<f4>(r, cf);
+        f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+        acc = fmac(acc, w0, img[(c01 & 0xffffu) * L + piece]);
+        acc = fmac(acc, w1, img[(c01 >> 16) * L + piece]);
+        acc = fmac(acc, w2, img[(c23 & 0xffffu) * L + piece]);
+        acc = fmac(acc, w3, img[(c23 >> 16) * L + piece]);
+        if (longm & (1u << k)) {  // long rows: the rest of the list from memory
+          const int e1 = rowptr[r + 1];
+          for (int e = rowptr[r] + DMAX; e < e1; ++e) acc = fmac(acc, val[e], img[col[e] * L + piece]);
+        }
+        acc = epi.apply(acc, es, r, cf);
+        char* yb = reinterpret_cast<char*>(Y + (int64_t(k * RSTEP + wrow) * ldy + s * L * 4));
+        stv<f4, NT_STORE>(reinterpret_cast<f4*>(yb + yoff), acc);
+      }
+      // one lane-row at a time: hoisting every row's LDS reads above the
+      // first store would need PER * DMAX * 4 live registers
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();
+  }
+}
+
+// ----------------------------------------------------------------------------
 // Fused prox / ADMM gradient term + momentum SGD.
 // MODE: 0 = no momentum, 1 = momentum first step (buf = g'), 2 = momentum.
 // ----------------------------------------------------------------------------
@@ -937,11 +1066,51 @@ int mix_csr_impl(const char* nm, const float* X, int64_t ldx, int32_t x_rows, fl
   const ColSplit cs = split_cols(P, vec_ok);
   constexpr int RPB = 16;
   constexpr int XW = 32, XPASSES = 2;  // XCD-pinned tiles: 512 B of a row, 16 rows per block
-  const int mode = env_int("DOL_CSR_MODE", -1);  // 0 = 4 KiB tiles, 1 = XCD-pinned
-  const bool use_xcd = cs.n4 >= XW && (mode == 1 || (mode < 0 && n_rows >= 512));
+  // 0 = 4 KiB tiles, 1 = XCD-pinned, 3 = LDS slab
+  const int mode = env_int("DOL_CSR_MODE", -1);
   if (cdiv(cs.n4, kThreads) * cdiv(n_rows, RPB) > kMaxBlocks)
     return fail(DOL_EINVAL, "%s: problem too large for one launch", nm);
   int64_t done4 = 0;
+  // LDS slab: the widest 16L-byte slab whose x_rows-row image fits 128 KiB
+  const int rows_max = std::max(n_rows, x_rows);
+  const int lds_l = rows_max <= 1024 ? 8 : rows_max <= 2048 ? 4 : rows_max <= 4096 ? 2 : rows_max <= 8192 ? 1 : 0;
+  static const int n_cu = [] {
+    int dev = 0, cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cu = 0;
+    return cu;
+  }();
+  // one workgroup per CU; DOL_CSR_LDS_GRID (a multiple of 8) overrides it so
+  // small test shapes exercise the kernel too
+  const int grid_env = env_int("DOL_CSR_LDS_GRID", 0);
+  const int lds_grid = grid_env >= 8 ? grid_env / 8 * 8 : (n_cu >= 8 ? n_cu / 8 * 8 : 0);
+  const bool use_lds = mode == 3 && lds_l > 0 && lds_grid > 0 && cs.n4 / lds_l >= lds_grid &&
+                       64 * std::max(ldx, ldy) * 4 < (int64_t(1) << 32);
+  if (use_lds) {
+    const int nt = env_int("DOL_CSR_LDS_NT", 1);
+    auto go = [&](auto lc, auto ntc) {
+      constexpr int Lc = decltype(lc)::value;
+      constexpr bool NTc = decltype(ntc)::value;
+      auto kern = csr_lds_kernel<Lc, kLdsT, NTc, Epi>;
+      constexpr int lds = kLdsSlabBytes + 16 * Lc;  // image + the zero row
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      const int64_t n_slabs = cs.n4 / Lc;
+      hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(lds_grid)), dim3(kLdsT), lds, s, X, ldx,
+                         x_rows, Y, ldy, n_rows, n_slabs, rowptr, col, val, epi);
+      done4 = n_slabs * Lc;
+    };
+    using std::integral_constant;
+    using T = integral_constant<bool, true>;
+    using F = integral_constant<bool, false>;
+    switch (lds_l) {
+      case 8: nt ? go(integral_constant<int, 8>{}, T{}) : go(integral_constant<int, 8>{}, F{}); break;
+      case 4: nt ? go(integral_constant<int, 4>{}, T{}) : go(integral_constant<int, 4>{}, F{}); break;
+      case 2: nt ? go(integral_constant<int, 2>{}, T{}) : go(integral_constant<int, 2>{}, F{}); break;
+      default: nt ? go(integral_constant<int, 1>{}, T{}) : go(integral_constant<int, 1>{}, F{}); break;
+    }
+  }
+  const bool use_xcd = !use_lds && cs.n4 >= XW && (mode == 1 || (mode < 0 && n_rows >= 512));
   if (use_xcd) {
     const int passes = env_int("DOL_CSR_PASSES", XPASSES);
     auto go = [&](auto pc) {
