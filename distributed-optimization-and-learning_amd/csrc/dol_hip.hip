@@ -491,44 +491,43 @@ __global__ __launch_bounds__(kThreads) void csr_xcd_kernel(
 }
 
 // ----------------------------------------------------------------------------
-// LDS-slab CSR mix (graphs of up to 8192 agents, any W): the whole column slab
-// X[0..x_rows)[16L bytes] lives in the CU's LDS (128 KiB), so every X byte is
-// read from memory ONCE per round however many rows gather it, and the deg
-// gathers per output row are LDS reads.  One persistent 1024-thread workgroup
-// per CU walks slabs; each thread owns PER = 8 lane-rows (row = k * 1024/L +
-// tid / L, 16-B piece tid % L) for the image fill AND for the output, and
-// keeps those rows' first DMAX neighbour indices / weights in registers for
-// the whole kernel (the index chain is paid once, not per tile).  The next
-// slab's X pieces are loaded into registers while the current slab's rows are
-// summed (register-staged double buffering; the image itself is single).
-// Slab order is XCD-aware: at step t, workgroup w of XCD x (= blockIdx % 8,
-// a speed assumption only) takes slab (t*8 + x)*nw + w: the workgroups of one
-// XCD hold adjacent slabs at the same moment, so the narrow row pieces they
-// read (16 B at 8192 agents) share L2 lines and DRAM pages.  Sums: +0 start, ascending CSR order, no
-// FMA — the same arithmetic as csr_mix_kernel (bit-identical).  Rows whose
-// degree exceeds DMAX read their extra (col, val) entries from memory.
+// LDS-slab CSR mix (graphs of up to 4096 agents, any W): the column slab
+// X[0..x_rows)[16L bytes] of every agent is staged in the CU's LDS, so each X
+// byte is read from memory ONCE per round however many rows gather it, and
+// the deg gathers per output row are LDS reads.  One persistent 1024-thread
+// workgroup per CU walks slabs with two 64 KiB images: the LDS-DMA
+// (global_load_lds_dwordx4, no registers) of slab t+1 flies while slab t is
+// summed.  Each thread owns PER = 4 lane-rows (row = k * 1024/L + tid / L,
+// 16-B piece tid % L) for the fill AND the output, and keeps those rows'
+// first four neighbour indices / weights in registers for the whole kernel
+// (the index chain is paid once, not per tile).  Slab order is XCD-aware: at
+// step t workgroup w of XCD x (= blockIdx % 8, a speed assumption only) takes
+// slab (t*8 + x)*nw + w, so one XCD's workgroups read adjacent pieces of the
+// same rows together.  Sums: +0 start, ascending CSR order, no FMA — the
+// arithmetic of csr_mix_kernel (bit-identical).  Rows with more than four
+// neighbours read the rest of their (col, val) list from memory.
 // ----------------------------------------------------------------------------
-constexpr int kLdsSlabBytes = 128 * 1024;
-constexpr int kLdsT = 1024;  // threads per LDS-slab workgroup
+constexpr int kLdsImgBytes = 64 * 1024;  // one image; two are double-buffered
+constexpr int kLdsT = 1024;              // threads per LDS-slab workgroup
 
-template <int L, int T, bool NT_STORE, class Epi = NoEpi>
-__global__ __launch_bounds__(T) void csr_lds_kernel(
+template <int L, bool NT_STORE, class Epi = NoEpi>
+__global__ __launch_bounds__(kLdsT) void csr_lds_kernel(
     const float* __restrict__ X, int64_t ldx, int x_rows, float* __restrict__ Y, int64_t ldy, int n_rows,
     int64_t n_slabs, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
     const float* __restrict__ val, Epi epi) {
-  constexpr int ROWS = kLdsSlabBytes / (16 * L);  // rows the image holds (8192 / L)
-  constexpr int RSTEP = T / L;                    // rows per lane-row step
-  constexpr int PER = ROWS / RSTEP;               // lane-rows per thread (8192 / T)
-  constexpr int DMAX = 4;                         // neighbours held in registers per row
-  static_assert(PER <= 32, "long-row flags must fit 32 bits");
-  // image rows [0, ROWS) + one zero row at ROWS: register slots past a row's
-  // degree point there with weight +0, and acc + (+0 * +0) == acc for every
-  // acc this sum can hold (it starts at +0 and so is never -0), so short
-  // rows need no per-entry branch
+  constexpr int ROWS = kLdsImgBytes / (16 * L);  // rows an image holds (4096 / L)
+  constexpr int RSTEP = kLdsT / L;               // rows per lane-row step
+  constexpr int PER = ROWS / RSTEP;              // lane-rows per thread (4)
+  constexpr int DMAX = 4;                        // neighbours held in registers per row
+  constexpr int IMG = (ROWS + 1) * L;            // f4 per image incl. its zero row
+  // two images, each followed by a zero row: register slots past a row's
+  // degree point at column ROWS (the zero row) with weight +0, and
+  // acc + (+0 * +0) == acc for every acc this sum can hold (it starts at +0,
+  // so it is never -0): short rows need no per-entry branch
   extern __shared__ __attribute__((aligned(16))) f4 img[];
   const int tid = threadIdx.x;
   const int piece = tid % L, rsub = tid / L;
-  if (tid < L) img[ROWS * L + tid] = f4{0.f, 0.f, 0.f, 0.f};
+  if (tid < 2 * L) img[(tid / L) * IMG + ROWS * L + tid % L] = f4{0.f, 0.f, 0.f, 0.f};
 
   uint32_t cc[PER][DMAX / 2];  // columns, two 16-bit indices per register
   float ww[PER][DMAX];
@@ -549,73 +548,141 @@ __global__ __launch_bounds__(T) void csr_lds_kernel(
       else cc[k][q / 2] |= cq << 16;
       ww[k][q] = in ? val[e] : 0.0f;
     }
-    __builtin_amdgcn_sched_barrier(0);  // bound the prologue's live addresses
   }
 
   const uint32_t xcd = blockIdx.x & 7u, wl = blockIdx.x >> 3, nw = gridDim.x >> 3;
   auto slab = [&](int64_t t) -> int64_t { return (t * 8 + xcd) * nw + wl; };
-  // addresses = wave-uniform 64-bit row base (SGPRs) + a 32-bit lane offset
-  // (lane's row within the wave * ld + piece; the host checks 64 * ld * 4 <
-  // 2^32), so no per-row 64-bit VGPR addresses stay live across the loop
+  // DMA sources = wave-uniform 64-bit row base + 32-bit lane offset (the host
+  // checks 64 * ld * 4 < 2^32).  Every lane loads, without a branch: a wave
+  // whose rows start past x_rows re-reads row x_rows - 1, a lane past x_rows
+  // its wave's first row, into image slots no column refers to.
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63;
   const int wrow = wave * (64 / L);  // the wave's first row within a step
   const uint32_t xoff = static_cast<uint32_t>(((lane / L) * ldx + piece * 4) * 4);
   const uint32_t yoff = static_cast<uint32_t>(((lane / L) * ldy + piece * 4) * 4);
-  f4 pf[PER];
-  // Every lane loads: a lane whose row is past x_rows re-reads its wave's
-  // first row (valid whenever the wave loads at all) into an image slot no
-  // column refers to, so the loads carry no per-lane branch.
-  auto fetch = [&](int64_t s) {
+  auto fill = [&](int64_t s, int b) {
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
-      if (k * RSTEP + wrow < x_rows) {  // wave-uniform
-        const char* wb = reinterpret_cast<const char*>(X + (int64_t(k * RSTEP + wrow) * ldx + s * L * 4));
-        const uint32_t o = k * RSTEP + rsub < x_rows ? xoff : static_cast<uint32_t>(piece * 16);
-        pf[k] = *reinterpret_cast<const f4*>(wb + o);
-      }
+      const int wr = min(k * RSTEP + wrow, x_rows - 1);
+      const uint32_t lo = k * RSTEP + rsub < x_rows ? xoff : static_cast<uint32_t>(piece * 16);
+      const char* src = reinterpret_cast<const char*>(X + (int64_t(wr) * ldx + s * L * 4)) + lo;
+      __builtin_amdgcn_global_load_lds(DOL_GPTR(src), DOL_LPTR(&img[b * IMG + (k * RSTEP + wrow) * L]), 16, 0, 0);
     }
   };
-  if (slab(0) < n_slabs) fetch(slab(0));
+  if (slab(0) < n_slabs) fill(slab(0), 0);
   for (int64_t t = 0;; ++t) {
     const int64_t s = slab(t);
     if (s >= n_slabs) break;
-#pragma unroll
-    for (int k = 0; k < PER; ++k)
-      if (k * RSTEP + wrow < x_rows) img[(k * RSTEP + rsub) * L + piece] = pf[k];
-    if (slab(t + 1) < n_slabs) fetch(slab(t + 1));
+    const int b = static_cast<int>(t & 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this slab's DMA (and the last slab's stores)
     __syncthreads();
+    if (slab(t + 1) < n_slabs) fill(slab(t + 1), b ^ 1);  // the image read two slabs ago
+    const f4* im = img + b * IMG;
     const int64_t cf = (s * L + piece) * 4;  // absolute float column of this lane's piece
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
       const int r = k * RSTEP + rsub;
       if (r < n_rows) {
-        // re-derive the LDS addresses each slab (an empty asm hides that they
-        // are loop-invariant: hoisted, they would cost PER * DMAX registers)
-        // (and the weights: the packed multiply wants each one duplicated
-        // into a register pair, which hoisted would double their footprint)
-        uint32_t c01 = cc[k][0], c23 = cc[k][1];
-        float w0 = ww[k][0], w1 = ww[k][1], w2 = ww[k][2], w3 = ww[k][3];
-        asm volatile("" : "+v"(c01), "+v"(c23), "+v"(w0), "+v"(w1), "+v"(w2), "+v"(w3));
         const auto es = epi.template load<f4>(r, cf);
         f4 acc = f4{0.f, 0.f, 0.f, 0.f};
-        acc = fmac(acc, w0, img[(c01 & 0xffffu) * L + piece]);
-        acc = fmac(acc, w1, img[(c01 >> 16) * L + piece]);
-        acc = fmac(acc, w2, img[(c23 & 0xffffu) * L + piece]);
-        acc = fmac(acc, w3, img[(c23 >> 16) * L + piece]);
+        acc = fmac(acc, ww[k][0], im[(cc[k][0] & 0xffffu) * L + piece]);
+        acc = fmac(acc, ww[k][1], im[(cc[k][0] >> 16) * L + piece]);
+        acc = fmac(acc, ww[k][2], im[(cc[k][1] & 0xffffu) * L + piece]);
+        acc = fmac(acc, ww[k][3], im[(cc[k][1] >> 16) * L + piece]);
         if (longm & (1u << k)) {  // long rows: the rest of the list from memory
           const int e1 = rowptr[r + 1];
-          for (int e = rowptr[r] + DMAX; e < e1; ++e) acc = fmac(acc, val[e], img[col[e] * L + piece]);
+          for (int e = rowptr[r] + DMAX; e < e1; ++e) acc = fmac(acc, val[e], im[col[e] * L + piece]);
         }
         acc = epi.apply(acc, es, r, cf);
         char* yb = reinterpret_cast<char*>(Y + (int64_t(k * RSTEP + wrow) * ldy + s * L * 4));
         stv<f4, NT_STORE>(reinterpret_cast<f4*>(yb + yoff), acc);
       }
-      // one lane-row at a time: hoisting every row's LDS reads above the
-      // first store would need PER * DMAX * 4 live registers
-      __builtin_amdgcn_sched_barrier(0);
     }
-    __syncthreads();
+  }
+}
+
+// ----------------------------------------------------------------------------
+// Persistent L2-gather CSR mix (large graphs, any W): one 1024-thread
+// workgroup per CU owns a fixed block of output rows and keeps their first
+// four neighbours' row offsets / weights in registers for the whole kernel;
+// the workgroups of XCD x walk column tiles x, x+8, x+16, ... (TW f4 = 16*TW
+// bytes of every row) in the same order, so one tile's slab (n x 16*TW B,
+// 1 MiB at 8192 agents and 128-B tiles) is fetched from HBM into that XCD's
+// L2 once and its deg re-reads hit there.  The next tile's gathers are issued
+// before the current tile's sums (register double buffer).  No index chain
+// per tile; the slab working set is two tiles.  Sums as csr_mix_kernel.
+// ----------------------------------------------------------------------------
+template <int TW, int RPT, class Epi = NoEpi>
+__global__ __launch_bounds__(1024) void csr_xcdp_kernel(
+    const float* __restrict__ X, int64_t ldx, float* __restrict__ Y, int64_t ldy, int n_rows, int rows_per_wg,
+    int64_t n_tiles, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
+    const float* __restrict__ val, Epi epi) {
+  constexpr int RSTEP = 1024 / TW;
+  constexpr int DMAX = 4;
+  const int tid = threadIdx.x;
+  const int piece = tid % TW, rsub = tid / TW;
+  const uint32_t xcd = blockIdx.x & 7u, wl = blockIdx.x >> 3;
+  const int row0 = static_cast<int>(wl) * rows_per_wg;
+  uint32_t off[RPT][DMAX];  // each neighbour row's offset (+ this lane's piece) in 16-B units
+  float ww[RPT][DMAX];
+  uint32_t dgm = 0;        // 4 bits per lane-row: min(degree, 15)
+#pragma unroll
+  for (int k = 0; k < RPT; ++k) {
+    const int r = row0 + k * RSTEP + rsub;
+    const bool live = r < n_rows && k * RSTEP + rsub < rows_per_wg;
+    const int rc = live ? r : 0;
+    const int e0 = rowptr[rc];
+    const int dg = live ? rowptr[rc + 1] - e0 : 0;
+    dgm |= uint32_t(dg < 15 ? dg : 15) << (4 * k);
+#pragma unroll
+    for (int q = 0; q < DMAX; ++q) {
+      const bool in = q < dg;
+      const int e = in ? e0 + q : 0;
+      off[k][q] = static_cast<uint32_t>((int64_t(in ? col[e] : 0) * ldx + piece * 4) / 4);
+      ww[k][q] = in ? val[e] : 0.0f;
+    }
+  }
+  f4 g[2][RPT][DMAX];
+  auto gather = [&](int64_t tile, f4 (&dst)[RPT][DMAX]) {
+    const char* base = reinterpret_cast<const char*>(X + tile * TW * 4);
+#pragma unroll
+    for (int k = 0; k < RPT; ++k)
+#pragma unroll
+      for (int q = 0; q < DMAX; ++q) dst[k][q] = *reinterpret_cast<const f4*>(base + uint64_t(off[k][q]) * 16);
+  };
+  auto finish = [&](int64_t tile, f4 (&src)[RPT][DMAX]) {
+    const int64_t cf = (tile * TW + piece) * 4;
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      const int r = row0 + k * RSTEP + rsub;
+      if (r < n_rows && k * RSTEP + rsub < rows_per_wg) {
+        const int dg = static_cast<int>((dgm >> (4 * k)) & 15u);
+        const auto es = epi.template load<f4>(r, cf);
+        f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int q = 0; q < DMAX; ++q) {
+          const f4 x = q < dg ? src[k][q] : f4{0.f, 0.f, 0.f, 0.f};  // +0 * +0: a no-op term
+          acc = fmac(acc, ww[k][q], x);
+        }
+        if (dg > DMAX) {
+          const int e1 = rowptr[r + 1];
+          for (int e = rowptr[r] + DMAX; e < e1; ++e)
+            acc = fmac(acc, val[e], *reinterpret_cast<const f4*>(X + int64_t(col[e]) * ldx + cf));
+        }
+        acc = epi.apply(acc, es, r, cf);
+        __builtin_nontemporal_store(acc, reinterpret_cast<f4*>(Y + int64_t(r) * ldy + cf));
+      }
+    }
+  };
+  int64_t t = xcd;
+  if (t < n_tiles) gather(t, g[0]);
+  for (; t < n_tiles; t += 16) {
+    if (t + 8 < n_tiles) gather(t + 8, g[1]);
+    finish(t, g[0]);
+    if (t + 8 >= n_tiles) break;
+    if (t + 16 < n_tiles) gather(t + 16, g[0]);
+    finish(t + 8, g[1]);
   }
 }
 
@@ -1071,9 +1138,9 @@ int mix_csr_impl(const char* nm, const float* X, int64_t ldx, int32_t x_rows, fl
   if (cdiv(cs.n4, kThreads) * cdiv(n_rows, RPB) > kMaxBlocks)
     return fail(DOL_EINVAL, "%s: problem too large for one launch", nm);
   int64_t done4 = 0;
-  // LDS slab: the widest 16L-byte slab whose x_rows-row image fits 128 KiB
+  // LDS slab: the widest 16L-byte slab whose x_rows-row image fits 64 KiB
   const int rows_max = std::max(n_rows, x_rows);
-  const int lds_l = rows_max <= 1024 ? 8 : rows_max <= 2048 ? 4 : rows_max <= 4096 ? 2 : rows_max <= 8192 ? 1 : 0;
+  const int lds_l = rows_max <= 512 ? 8 : rows_max <= 1024 ? 4 : rows_max <= 2048 ? 2 : rows_max <= 4096 ? 1 : 0;
   static const int n_cu = [] {
     int dev = 0, cu = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
@@ -1088,12 +1155,12 @@ int mix_csr_impl(const char* nm, const float* X, int64_t ldx, int32_t x_rows, fl
   const bool use_lds = mode == 3 && lds_l > 0 && lds_grid > 0 && cs.n4 / lds_l >= lds_grid &&
                        64 * std::max(ldx, ldy) * 4 < (int64_t(1) << 32);
   if (use_lds) {
-    const int nt = env_int("DOL_CSR_LDS_NT", 1);
+    const int nt = env_int("DOL_CSR_LDS_NT", 0);
     auto go = [&](auto lc, auto ntc) {
       constexpr int Lc = decltype(lc)::value;
       constexpr bool NTc = decltype(ntc)::value;
-      auto kern = csr_lds_kernel<Lc, kLdsT, NTc, Epi>;
-      constexpr int lds = kLdsSlabBytes + 16 * Lc;  // image + the zero row
+      auto kern = csr_lds_kernel<Lc, NTc, Epi>;
+      constexpr int lds = 2 * (kLdsImgBytes + 16 * Lc);  // two images, each with its zero row
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
       const int64_t n_slabs = cs.n4 / Lc;
       hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(lds_grid)), dim3(kLdsT), lds, s, X, ldx,
@@ -1110,7 +1177,29 @@ int mix_csr_impl(const char* nm, const float* X, int64_t ldx, int32_t x_rows, fl
       default: nt ? go(integral_constant<int, 1>{}, T{}) : go(integral_constant<int, 1>{}, F{}); break;
     }
   }
-  const bool use_xcd = !use_lds && cs.n4 >= XW && (mode == 1 || (mode < 0 && n_rows >= 512));
+  const int tw = env_int("DOL_CSR_XCDP_TW", 8);
+  const bool use_xcdp = !use_lds && mode == 4 && lds_grid > 0 && cs.n4 >= 8 * tw;
+  if (use_xcdp) {
+    auto go = [&](auto twc, auto rptc) {
+      constexpr int TWc = decltype(twc)::value, RPTc = decltype(rptc)::value;
+      const int nw = lds_grid / 8;
+      const int rpw = static_cast<int>(cdiv(n_rows, nw));
+      if (rpw > RPTc * (1024 / TWc)) return false;
+      const int64_t nt = cs.n4 / TWc;
+      hipLaunchKernelGGL((csr_xcdp_kernel<TWc, RPTc, Epi>), dim3(static_cast<unsigned>(lds_grid)), dim3(1024), 0, s,
+                         X, ldx, Y, ldy, n_rows, rpw, nt, rowptr, col, val, epi);
+      done4 = nt * TWc;
+      return true;
+    };
+    using std::integral_constant;
+    bool ok = false;
+    if (int64_t(x_rows) * ldx / 4 >= (int64_t(1) << 32))
+      return fail(DOL_EINVAL, "%s: DOL_CSR_MODE=4: X too large for 32-bit row offsets", nm);
+    if (tw == 4) ok = go(integral_constant<int, 4>{}, integral_constant<int, 1>{});
+    else ok = go(integral_constant<int, 8>{}, integral_constant<int, 2>{});
+    if (!ok) return fail(DOL_EINVAL, "%s: DOL_CSR_MODE=4: too many rows per workgroup", nm);
+  }
+  const bool use_xcd = !use_lds && !use_xcdp && cs.n4 >= XW && (mode == 1 || (mode < 0 && n_rows >= 512));
   if (use_xcd) {
     const int passes = env_int("DOL_CSR_PASSES", XPASSES);
     auto go = [&](auto pc) {
