@@ -603,6 +603,100 @@ __global__ __launch_bounds__(kLdsT) void csr_lds_kernel(
 }
 
 // ----------------------------------------------------------------------------
+// LDS-slab CSR mix, register-staged, for graphs of up to 1024 agents: one
+// 128-B column slab of every agent (128 KiB) plus the whole graph's index
+// (first four columns as u16, weights as fp32: 24 KiB) live in LDS.  One
+// persistent 1024-thread workgroup per CU; each thread owns 8 lane-rows
+// (row = k * 128 + tid / 8, 16-B piece tid % 8) for the fill and the output.
+// The next slab is loaded into registers while the current one is summed.
+// Column 1024 is an all-zero row that pads short rows (see csr_lds_kernel);
+// bit 15 of a row's first column marks a row with more than four neighbours,
+// whose remaining entries come from memory.  Sums as csr_mix_kernel.
+// ----------------------------------------------------------------------------
+constexpr int kLds8Rows = 1024;
+constexpr int kLds8Bytes = (kLds8Rows + 1) * 128 + kLds8Rows * (16 + 8);
+
+template <bool NT_STORE, class Epi = NoEpi>
+__global__ __launch_bounds__(1024) void csr_lds8_kernel(
+    const float* __restrict__ X, int64_t ldx, int x_rows, float* __restrict__ Y, int64_t ldy, int n_rows,
+    int64_t n_slabs, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
+    const float* __restrict__ val, Epi epi) {
+  constexpr int L = 8, RSTEP = 128, PER = 8, ZROW = kLds8Rows;
+  extern __shared__ __attribute__((aligned(16))) f4 img[];  // [(1024 + 1) * 8]
+  f4* wts = img + (kLds8Rows + 1) * L;                        // [1024] x 4 weights
+  uint2* cols = reinterpret_cast<uint2*>(wts + kLds8Rows);    // [1024] x 4 u16 columns
+  const int tid = threadIdx.x;
+  const int piece = tid % L, rsub = tid / L;
+  if (tid < L) img[ZROW * L + tid] = f4{0.f, 0.f, 0.f, 0.f};
+  {  // the graph's index: thread tid stages row tid
+    const int r = tid;
+    const int e0 = r < n_rows ? rowptr[r] : 0;
+    const int dg = r < n_rows ? rowptr[r + 1] - e0 : 0;
+    uint32_t c[4];
+    float w[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const bool in = q < dg;
+      c[q] = in ? static_cast<uint32_t>(col[e0 + q]) : uint32_t(ZROW);
+      w[q] = in ? val[e0 + q] : 0.0f;
+    }
+    if (dg > 4) c[0] |= 0x8000u;
+    wts[r] = f4{w[0], w[1], w[2], w[3]};
+    cols[r] = uint2{c[0] | (c[1] << 16), c[2] | (c[3] << 16)};
+  }
+  const uint32_t xcd = blockIdx.x & 7u, wl = blockIdx.x >> 3, nw = gridDim.x >> 3;
+  auto slab = [&](int64_t t) -> int64_t { return (t * 8 + xcd) * nw + wl; };
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63;
+  const int wrow = wave * (64 / L);
+  const uint32_t xoff = static_cast<uint32_t>(((lane / L) * ldx + piece * 4) * 4);
+  const uint32_t yoff = static_cast<uint32_t>(((lane / L) * ldy + piece * 4) * 4);
+  f4 pf[PER];
+  // every lane loads, without a branch (rows past x_rows: see csr_lds_kernel)
+  auto fetch = [&](int64_t s) {
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int wr = min(k * RSTEP + wrow, x_rows - 1);
+      const uint32_t lo = k * RSTEP + rsub < x_rows ? xoff : static_cast<uint32_t>(piece * 16);
+      pf[k] = *reinterpret_cast<const f4*>(reinterpret_cast<const char*>(X + (int64_t(wr) * ldx + s * L * 4)) + lo);
+    }
+  };
+  if (slab(0) < n_slabs) fetch(slab(0));
+  for (int64_t t = 0;; ++t) {
+    const int64_t s = slab(t);
+    if (s >= n_slabs) break;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) img[(k * RSTEP + rsub) * L + piece] = pf[k];
+    if (slab(t + 1) < n_slabs) fetch(slab(t + 1));
+    __syncthreads();
+    const int64_t cf = (s * L + piece) * 4;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int r = k * RSTEP + rsub;
+      if (r < n_rows) {
+        const uint2 c = cols[r];
+        const f4 w = wts[r];
+        const auto es = epi.template load<f4>(r, cf);
+        f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+        acc = fmac(acc, w.x, img[(c.x & 0x7fffu) * L + piece]);
+        acc = fmac(acc, w.y, img[(c.x >> 16) * L + piece]);
+        acc = fmac(acc, w.z, img[(c.y & 0xffffu) * L + piece]);
+        acc = fmac(acc, w.w, img[(c.y >> 16) * L + piece]);
+        if (c.x & 0x8000u) {  // long rows: the rest of the list from memory
+          const int e1 = rowptr[r + 1];
+          for (int e = rowptr[r] + 4; e < e1; ++e) acc = fmac(acc, val[e], img[col[e] * L + piece]);
+        }
+        acc = epi.apply(acc, es, r, cf);
+        char* yb = reinterpret_cast<char*>(Y + (int64_t(k * RSTEP + wrow) * ldy + s * L * 4));
+        stv<f4, NT_STORE>(reinterpret_cast<f4*>(yb + yoff), acc);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();
+  }
+}
+
+// ----------------------------------------------------------------------------
 // Persistent L2-gather CSR mix (large graphs, any W): one 1024-thread
 // workgroup per CU owns a fixed block of output rows and keeps their first
 // four neighbours' row offsets / weights in registers for the whole kernel;
@@ -1177,8 +1271,23 @@ int mix_csr_impl(const char* nm, const float* X, int64_t ldx, int32_t x_rows, fl
       default: nt ? go(integral_constant<int, 1>{}, T{}) : go(integral_constant<int, 1>{}, F{}); break;
     }
   }
+  const bool use_lds8 = !use_lds && mode == 5 && rows_max <= kLds8Rows && lds_grid > 0 && cs.n4 / 8 >= lds_grid &&
+                        64 * std::max(ldx, ldy) * 4 < (int64_t(1) << 32);
+  if (use_lds8) {
+    auto go = [&](auto ntc) {
+      auto kern = csr_lds8_kernel<decltype(ntc)::value, Epi>;
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                kLds8Bytes);
+      const int64_t n_slabs = cs.n4 / 8;
+      hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(lds_grid)), dim3(1024), kLds8Bytes, s, X, ldx, x_rows, Y,
+                         ldy, n_rows, n_slabs, rowptr, col, val, epi);
+      done4 = n_slabs * 8;
+    };
+    if (env_int("DOL_CSR_LDS_NT", 0)) go(std::integral_constant<bool, true>{});
+    else go(std::integral_constant<bool, false>{});
+  }
   const int tw = env_int("DOL_CSR_XCDP_TW", 8);
-  const bool use_xcdp = !use_lds && mode == 4 && lds_grid > 0 && cs.n4 >= 8 * tw;
+  const bool use_xcdp = !use_lds && !use_lds8 && mode == 4 && lds_grid > 0 && cs.n4 >= 8 * tw;
   if (use_xcdp) {
     auto go = [&](auto twc, auto rptc) {
       constexpr int TWc = decltype(twc)::value, RPTc = decltype(rptc)::value;
@@ -1199,7 +1308,7 @@ int mix_csr_impl(const char* nm, const float* X, int64_t ldx, int32_t x_rows, fl
     else ok = go(integral_constant<int, 8>{}, integral_constant<int, 2>{});
     if (!ok) return fail(DOL_EINVAL, "%s: DOL_CSR_MODE=4: too many rows per workgroup", nm);
   }
-  const bool use_xcd = !use_lds && !use_xcdp && cs.n4 >= XW && (mode == 1 || (mode < 0 && n_rows >= 512));
+  const bool use_xcd = !use_lds && !use_lds8 && !use_xcdp && cs.n4 >= XW && (mode == 1 || (mode < 0 && n_rows >= 512));
   if (use_xcd) {
     const int passes = env_int("DOL_CSR_PASSES", XPASSES);
     auto go = [&](auto pc) {
