@@ -697,6 +697,94 @@ __global__ __launch_bounds__(1024) void csr_lds8_kernel(
 }
 
 // ----------------------------------------------------------------------------
+// Two-workgroups-per-CU form of csr_lds8_kernel for graphs of up to 1024
+// agents: 64-B slabs (a 64 KiB image per workgroup), the rows' first four
+// neighbours in registers, 512 threads x 8 lane-rows; while one workgroup
+// waits at its barrier the other streams.  Same arithmetic (bit-identical).
+// ----------------------------------------------------------------------------
+template <bool NT_STORE, class Epi = NoEpi>
+__global__ __launch_bounds__(512, 2) void csr_lds2w_kernel(
+    const float* __restrict__ X, int64_t ldx, int x_rows, float* __restrict__ Y, int64_t ldy, int n_rows,
+    int64_t n_slabs, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
+    const float* __restrict__ val, Epi epi) {
+  constexpr int L = 4, T = 512, ROWS = 1024, RSTEP = T / L, PER = ROWS / RSTEP, ZROW = ROWS;
+  extern __shared__ __attribute__((aligned(16))) f4 img[];  // [(1024 + 1) * 4]
+  const int tid = threadIdx.x;
+  const int piece = tid % L, rsub = tid / L;
+  if (tid < L) img[ZROW * L + tid] = f4{0.f, 0.f, 0.f, 0.f};
+  uint32_t cc[PER][2];
+  float ww[PER][4];
+  uint32_t longm = 0;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int r = k * RSTEP + rsub;
+    const int e0 = r < n_rows ? rowptr[r] : 0;
+    const int dg = r < n_rows ? rowptr[r + 1] - e0 : 0;
+    longm |= uint32_t(dg > 4) << k;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const bool in = q < dg;
+      const uint32_t cq = in ? static_cast<uint32_t>(col[e0 + q]) : uint32_t(ZROW);
+      if (q % 2 == 0) cc[k][q / 2] = cq;
+      else cc[k][q / 2] |= cq << 16;
+      ww[k][q] = in ? val[e0 + q] : 0.0f;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  const uint32_t xcd = blockIdx.x & 7u, wl = blockIdx.x >> 3, nw = gridDim.x >> 3;
+  auto slab = [&](int64_t t) -> int64_t { return (t * 8 + xcd) * nw + wl; };
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63;
+  const int wrow = wave * (64 / L);
+  const uint32_t xoff = static_cast<uint32_t>(((lane / L) * ldx + piece * 4) * 4);
+  const uint32_t yoff = static_cast<uint32_t>(((lane / L) * ldy + piece * 4) * 4);
+  f4 pf[PER];
+  auto fetch = [&](int64_t s) {
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int wr = min(k * RSTEP + wrow, x_rows - 1);
+      uint32_t lo = k * RSTEP + rsub < x_rows ? xoff : static_cast<uint32_t>(piece * 16);
+      asm volatile("" : "+v"(lo));
+      pf[k] = *reinterpret_cast<const f4*>(reinterpret_cast<const char*>(X + (int64_t(wr) * ldx + s * L * 4)) + lo);
+    }
+  };
+  if (slab(0) < n_slabs) fetch(slab(0));
+  for (int64_t t = 0;; ++t) {
+    const int64_t s = slab(t);
+    if (s >= n_slabs) break;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) img[(k * RSTEP + rsub) * L + piece] = pf[k];
+    if (slab(t + 1) < n_slabs) fetch(slab(t + 1));
+    __syncthreads();
+    const int64_t cf = (s * L + piece) * 4;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int r = k * RSTEP + rsub;
+      if (r < n_rows) {
+        uint32_t c01 = cc[k][0], c23 = cc[k][1];
+        float w0 = ww[k][0], w1 = ww[k][1], w2 = ww[k][2], w3 = ww[k][3];
+        asm volatile("" : "+v"(c01), "+v"(c23), "+v"(w0), "+v"(w1), "+v"(w2), "+v"(w3));
+        const auto es = epi.template load<f4>(r, cf);
+        f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+        acc = fmac(acc, w0, img[(c01 & 0xffffu) * L + piece]);
+        acc = fmac(acc, w1, img[(c01 >> 16) * L + piece]);
+        acc = fmac(acc, w2, img[(c23 & 0xffffu) * L + piece]);
+        acc = fmac(acc, w3, img[(c23 >> 16) * L + piece]);
+        if (longm & (1u << k)) {
+          const int e1 = rowptr[r + 1];
+          for (int e = rowptr[r] + 4; e < e1; ++e) acc = fmac(acc, val[e], img[col[e] * L + piece]);
+        }
+        acc = epi.apply(acc, es, r, cf);
+        char* yb = reinterpret_cast<char*>(Y + (int64_t(k * RSTEP + wrow) * ldy + s * L * 4));
+        stv<f4, NT_STORE>(reinterpret_cast<f4*>(yb + yoff), acc);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();
+  }
+}
+
+// ----------------------------------------------------------------------------
 // Persistent L2-gather CSR mix (large graphs, any W): one 1024-thread
 // workgroup per CU owns a fixed block of output rows and keeps their first
 // four neighbours' row offsets / weights in registers for the whole kernel;
@@ -948,6 +1036,110 @@ __global__ __launch_bounds__(kThreads) void resid_reduce_kernel(const double* __
   for (int64_t i = threadIdx.x; i < n_chunks; i += kThreads) v += partial[agent * n_chunks + i];
   const double s = block_sum_f64(v, smem);
   if (threadIdx.x == 0) out[agent] = s;
+}
+
+// ----------------------------------------------------------------------------
+// One FedADMM client round on the separable least-squares objective
+// f_k(w) = 1/2 ||w - t_k||^2 (BASELINE config 4's primal/dual side), fused
+// per sampled agent k (row a = agents[k]) — the reference's
+// FedAdmm_Client.update_weights (DEC/clients.py:36-53) with the CNN gradient
+// replaced by the exact least-squares one:
+//   w = theta                                   (load_state_dict(theta), :37)
+//   local_steps times:  g = fl(w - t)
+//     g' = fl(g + fl(alpha + fl(rho * fl(w - theta))))        (:132-135)
+//     SGD(lr, momentum).step(): buf = first ? g' : fl(fl(buf*mu) + g'); w = fma(-lr, buf, w)
+//   alpha = fl(alpha + fl(rho * fl(w - theta)))  (update_duals, :141-144, pre-round theta)
+// Streams t, alpha (, buf) in and w, alpha (, buf) out once; w is never read.
+// RESID: fp64 per-block partials of ||w - theta||^2 and ||alpha||^2 (fixed
+// reduction tree, deterministic), as admm_dual_kernel.
+// ----------------------------------------------------------------------------
+template <bool MOM>
+__device__ __forceinline__ void admm_ls_lane(float& w, float& b, float& a, float t, float th, float rho,
+                                             float neg_lr, float mom, int steps, bool first, double& rw,
+                                             double& ra) {
+  w = th;
+  for (int k = 0; k < steps; ++k) {
+    const float g = w - t;
+    const float gg = g + (a + rho * (w - th));
+    float d = gg;
+    if constexpr (MOM) {
+      b = (first && k == 0) ? gg : b * mom + gg;
+      d = b;
+    }
+    w = __builtin_fmaf(neg_lr, d, w);
+  }
+  const float dl = w - th;
+  a = a + rho * dl;
+  rw += double(dl) * double(dl);
+  ra += double(a) * double(a);
+}
+
+template <bool VEC, bool MOM, bool RESID>
+__global__ __launch_bounds__(kThreads) void admm_ls_round_kernel(
+    float* __restrict__ W, int64_t ldw, float* __restrict__ B, int64_t ldb, float* __restrict__ A, int64_t lda,
+    const float* __restrict__ T, int64_t ldt, const float* __restrict__ theta, const int32_t* __restrict__ agents,
+    const int32_t* __restrict__ first, int64_t P, float rho, float neg_lr, float mom, int steps, int64_t n_chunks,
+    double* __restrict__ partial) {
+  __shared__ double smem[kThreads / 64];
+  const int64_t blk = blockIdx.x;
+  const int64_t k = blk / n_chunks;
+  const int64_t chunk = blk % n_chunks;
+  const int64_t a_row = agents ? agents[k] : k;
+  const bool fst = first ? first[k] != 0 : false;
+  float* wr = W + a_row * ldw;
+  float* br = B + a_row * ldb;
+  float* ar = A + a_row * lda;
+  const float* tr = T + a_row * ldt;
+  double rw = 0.0, ra = 0.0;
+  auto one = [&](int64_t c) {
+    float w, b = MOM ? br[c] : 0.0f, a = ar[c];
+    admm_ls_lane<MOM>(w, b, a, tr[c], theta[c], rho, neg_lr, mom, steps, fst, rw, ra);
+    wr[c] = w;
+    ar[c] = a;
+    if constexpr (MOM) br[c] = b;
+  };
+  if constexpr (VEC) {
+    const int64_t n4 = P / 4;
+#pragma unroll
+    for (int it = 0; it < kDualIters; ++it) {
+      const int64_t c = (chunk * kDualIters + it) * kThreads + threadIdx.x;
+      if (c < n4) {
+        const f4 t = reinterpret_cast<const f4*>(tr)[c];
+        const f4 th = reinterpret_cast<const f4*>(theta)[c];
+        f4 a = reinterpret_cast<const f4*>(ar)[c];
+        f4 b = MOM ? reinterpret_cast<const f4*>(br)[c] : f4{0.f, 0.f, 0.f, 0.f};
+        f4 w;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float wj, bj = b[j], aj = a[j];
+          admm_ls_lane<MOM>(wj, bj, aj, t[j], th[j], rho, neg_lr, mom, steps, fst, rw, ra);
+          w[j] = wj;
+          b[j] = bj;
+          a[j] = aj;
+        }
+        reinterpret_cast<f4*>(wr)[c] = w;
+        reinterpret_cast<f4*>(ar)[c] = a;
+        if constexpr (MOM) reinterpret_cast<f4*>(br)[c] = b;
+      }
+    }
+    const int64_t tail = P - 4 * n4;
+    if (chunk == n_chunks - 1 && threadIdx.x < tail) one(4 * n4 + threadIdx.x);
+  } else {
+#pragma unroll
+    for (int it = 0; it < kDualIters; ++it) {
+      const int64_t c = (chunk * kDualIters + it) * kThreads + threadIdx.x;
+      if (c < P) one(c);
+    }
+  }
+  if constexpr (RESID) {
+    const double sw = block_sum_f64(rw, smem);
+    __syncthreads();
+    const double sa = block_sum_f64(ra, smem);
+    if (threadIdx.x == 0) {
+      partial[k * n_chunks + chunk] = sw;
+      partial[(gridDim.x / n_chunks + k) * n_chunks + chunk] = sa;
+    }
+  }
 }
 
 // ----------------------------------------------------------------------------
@@ -1286,8 +1478,23 @@ int mix_csr_impl(const char* nm, const float* X, int64_t ldx, int32_t x_rows, fl
     if (env_int("DOL_CSR_LDS_NT", 0)) go(std::integral_constant<bool, true>{});
     else go(std::integral_constant<bool, false>{});
   }
+  const bool use_lds2w = !use_lds && !use_lds8 && mode == 6 && rows_max <= 1024 && lds_grid > 0 &&
+                         cs.n4 / 4 >= 2 * lds_grid && 64 * std::max(ldx, ldy) * 4 < (int64_t(1) << 32);
+  if (use_lds2w) {
+    auto go = [&](auto ntc) {
+      auto kern = csr_lds2w_kernel<decltype(ntc)::value, Epi>;
+      constexpr int lds = (1024 + 1) * 64;
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      const int64_t n_slabs = cs.n4 / 4;
+      hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(2 * lds_grid)), dim3(512), lds, s, X, ldx, x_rows, Y, ldy,
+                         n_rows, n_slabs, rowptr, col, val, epi);
+      done4 = n_slabs * 4;
+    };
+    if (env_int("DOL_CSR_LDS_NT", 0)) go(std::integral_constant<bool, true>{});
+    else go(std::integral_constant<bool, false>{});
+  }
   const int tw = env_int("DOL_CSR_XCDP_TW", 8);
-  const bool use_xcdp = !use_lds && !use_lds8 && mode == 4 && lds_grid > 0 && cs.n4 >= 8 * tw;
+  const bool use_xcdp = !use_lds && !use_lds8 && !use_lds2w && mode == 4 && lds_grid > 0 && cs.n4 >= 8 * tw;
   if (use_xcdp) {
     auto go = [&](auto twc, auto rptc) {
       constexpr int TWc = decltype(twc)::value, RPTc = decltype(rptc)::value;
@@ -1308,7 +1515,7 @@ int mix_csr_impl(const char* nm, const float* X, int64_t ldx, int32_t x_rows, fl
     else ok = go(integral_constant<int, 8>{}, integral_constant<int, 2>{});
     if (!ok) return fail(DOL_EINVAL, "%s: DOL_CSR_MODE=4: too many rows per workgroup", nm);
   }
-  const bool use_xcd = !use_lds && !use_lds8 && !use_xcdp && cs.n4 >= XW && (mode == 1 || (mode < 0 && n_rows >= 512));
+  const bool use_xcd = !use_lds && !use_lds8 && !use_lds2w && !use_xcdp && cs.n4 >= XW && (mode == 1 || (mode < 0 && n_rows >= 512));
   if (use_xcd) {
     const int passes = env_int("DOL_CSR_PASSES", XPASSES);
     auto go = [&](auto pc) {
@@ -1661,6 +1868,60 @@ int dol_admm_dual_f32(float* alpha, int64_t lda, const float* w, int64_t ldw, co
     else hipLaunchKernelGGL((admm_dual_kernel<false, false>), grid, dim3(kThreads), 0, s, alpha, lda, w, ldw, theta, rho, P, chunks, partial);
   }
   return check_launch("dol_admm_dual_f32");
+}
+
+int64_t dol_admm_ls_round_workspace_bytes(int32_t m, int64_t P) {
+  if (m <= 0 || P <= 0) return 0;
+  return 2 * dol_admm_dual_workspace_bytes(m, P);  // ||w - theta||^2 and ||alpha||^2 partials
+}
+
+int dol_admm_ls_round_f32(float* w, int64_t ldw, float* buf, int64_t ldb, float* alpha, int64_t lda,
+                          const float* target, int64_t ldt, const float* theta, const int32_t* agents,
+                          const int32_t* first, int32_t m, int64_t P, float rho, float lr, float momentum,
+                          int32_t local_steps, double* resid_sq, double* alpha_sq, void* work, hipStream_t s) {
+  const char* nm = "dol_admm_ls_round_f32";
+  if (m < 0 || P < 0 || local_steps < 0) return fail(DOL_EINVAL, "%s: negative size", nm);
+  if (m == 0) { g_err[0] = '\0'; return DOL_OK; }
+  const bool mom = momentum != 0.0f;
+  if (P > 0 && (!w || !alpha || !target || !theta || (mom && !buf))) return fail(DOL_EINVAL, "%s: null pointer", nm);
+  if ((resid_sq == nullptr) != (alpha_sq == nullptr)) return fail(DOL_EINVAL, "%s: pass both residual outputs or neither", nm);
+  if (resid_sq && !work && P > 0) return fail(DOL_EINVAL, "%s: residuals need a workspace", nm);
+  if (ldw < P || lda < P || ldt < P || (mom && ldb < P)) return fail(DOL_EINVAL, "%s: ld < P", nm);
+  if (P == 0) {
+    if (resid_sq) {
+      (void)hipMemsetAsync(resid_sq, 0, sizeof(double) * m, s);
+      (void)hipMemsetAsync(alpha_sq, 0, sizeof(double) * m, s);
+    }
+    return check_launch(nm);
+  }
+  const bool vec = row_vec_ok(w, ldw) && row_vec_ok(alpha, lda) && row_vec_ok(target, ldt) && row_vec_ok(theta, 0) &&
+                   (!mom || row_vec_ok(buf, ldb));
+  const int64_t per_block = int64_t(kThreads) * kDualIters;
+  const int64_t chunks = vec ? std::max<int64_t>(1, cdiv(P / 4, per_block)) : cdiv(P, per_block);
+  if (chunks * m > kMaxBlocks) return fail(DOL_EINVAL, "%s: problem too large", nm);
+  double* partial = static_cast<double*>(work);
+  const dim3 grid(static_cast<unsigned>(chunks * m));
+  auto go = [&](auto vc, auto mc, auto rc) {
+    hipLaunchKernelGGL((admm_ls_round_kernel<decltype(vc)::value, decltype(mc)::value, decltype(rc)::value>), grid,
+                       dim3(kThreads), 0, s, w, ldw, buf, ldb, alpha, lda, target, ldt, theta, agents, first, P, rho,
+                       -lr, momentum, local_steps, chunks, partial);
+  };
+  using std::integral_constant;
+  using Tb = integral_constant<bool, true>;
+  using Fb = integral_constant<bool, false>;
+  if (vec) {
+    if (mom) { if (resid_sq) go(Tb{}, Tb{}, Tb{}); else go(Tb{}, Tb{}, Fb{}); }
+    else { if (resid_sq) go(Tb{}, Fb{}, Tb{}); else go(Tb{}, Fb{}, Fb{}); }
+  } else {
+    if (mom) { if (resid_sq) go(Fb{}, Tb{}, Tb{}); else go(Fb{}, Tb{}, Fb{}); }
+    else { if (resid_sq) go(Fb{}, Fb{}, Tb{}); else go(Fb{}, Fb{}, Fb{}); }
+  }
+  if (resid_sq) {
+    hipLaunchKernelGGL(resid_reduce_kernel, dim3(m), dim3(kThreads), 0, s, partial, chunks, resid_sq);
+    hipLaunchKernelGGL(resid_reduce_kernel, dim3(m), dim3(kThreads), 0, s, partial + int64_t(m) * chunks, chunks,
+                       alpha_sq);
+  }
+  return check_launch(nm);
 }
 
 int dol_ordered_sum_f32(const float* W, int64_t ldw, const int32_t* order, int32_t m, int64_t P,

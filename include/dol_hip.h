@@ -215,6 +215,32 @@ int dol_admm_dual_f32(float* alpha, int64_t lda, const float* w, int64_t ldw,
 int64_t dol_admm_dual_workspace_bytes(int32_t n_agents, int64_t P);
 
 /*
+ * One FedADMM client round for m sampled agents on the separable least-squares
+ * objective f_k(w) = 1/2 ||w - t_k||^2 (BASELINE config 4's primal/dual side),
+ * fused into one pass per agent.  Replaces FedAdmm_Client.update_weights
+ * (DEC/clients.py:36-53) with the CNN gradient swapped for the exact
+ * least-squares one, for agent row a = agents[k] (agents NULL: a = k):
+ *   w = theta                                                    (:37)
+ *   local_steps times:  g = fl(w - t_a)
+ *     g' = fl(g + fl(alpha + fl(rho * fl(w - theta))))           (:132-135)
+ *     momentum != 0: buf = (first[k] && step 0) ? g' : fl(fl(buf*momentum) + g'); d = buf
+ *     momentum == 0: d = g'
+ *     w = fma(-lr, d, w)                                         (SGD.step, :44)
+ *   alpha = fl(alpha + fl(rho * fl(w - theta)))                  (update_duals, :141-144)
+ * first: [m] nonzero where agent k takes its first momentum step ever (the
+ * reference's optimizer state is never reset), or NULL for none.  w is only
+ * written.  resid_sq / alpha_sq (both or neither, fp64 [m]) receive
+ * ||w_k - theta||^2 and ||alpha_k||^2 after the round, summed in a fixed order;
+ * they need `work` of dol_admm_ls_round_workspace_bytes(m, P) bytes.  The
+ * server's average of the new w rows is dol_ordered_mean_f32 (DEC/servers.py:42-48).
+ */
+int dol_admm_ls_round_f32(float* w, int64_t ldw, float* buf, int64_t ldb, float* alpha, int64_t lda,
+                          const float* target, int64_t ldt, const float* theta, const int32_t* agents,
+                          const int32_t* first, int32_t m, int64_t P, float rho, float lr, float momentum,
+                          int32_t local_steps, double* resid_sq, double* alpha_sq, void* work, hipStream_t s);
+int64_t dol_admm_ls_round_workspace_bytes(int32_t m, int64_t P);
+
+/*
  * Ordered uniform average, replacing Server.average_weights
  *   DEC/servers.py:42-48:  acc = w[order[0]]; acc = fl(acc + w[order[k]]) k=1..m-1;
  *                          theta = fl(acc / (float)m)

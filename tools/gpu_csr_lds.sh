@@ -11,7 +11,7 @@ runt() {
 if [ -z "$NO_TESTS" ]; then
   DOL_CSR_MODE=3 DOL_CSR_LDS_GRID=16 runt > gpurun_out/csr_t3.log 2>&1; rc=$?; tail -1 gpurun_out/csr_t3.log; [ $rc -eq 0 ] || exit $rc
   DOL_CSR_MODE=5 DOL_CSR_LDS_GRID=16 runt > gpurun_out/csr_t5.log 2>&1; rc=$?; tail -1 gpurun_out/csr_t5.log; [ $rc -eq 0 ] || exit $rc
-  DOL_CSR_MODE=4 DOL_CSR_LDS_GRID=64 DOL_CSR_XCDP_TW=4 runt > gpurun_out/csr_t4b.log 2>&1; rc=$?; tail -1 gpurun_out/csr_t4b.log; [ $rc -eq 0 ] || exit $rc
+  DOL_CSR_MODE=6 DOL_CSR_LDS_GRID=16 runt > gpurun_out/csr_t6.log 2>&1; rc=$?; tail -1 gpurun_out/csr_t6.log; [ $rc -eq 0 ] || exit $rc
 fi
 for cfg in ${CFGS:-"1_8" "3_8" "4_8" "4_4" "1_8" "3_8" "4_8" "4_4"}; do
   m=${cfg%_*}; tw=${cfg#*_}
