@@ -1,0 +1,342 @@
+// pmajor.hip — the sparse gossip mix on the PARAMETER-MAJOR ("transposed")
+// bank layout, and the layout conversion.  Part of libdol_hip.so.
+//
+// Layout.  The agent-major bank (row k = agent k's P parameters, dol_hip.hip)
+// is what the notebooks' nn.Module views need.  For synthetic many-agent
+// workloads whose local steps are per coordinate (BASELINE config 3: 1024-8192
+// agents x 2^20 on a random-regular W) the engine can hold the bank
+// transposed instead: XT[p][j] = agent j's parameter p, p-row stride ldx >= N.
+// One p-row is then the whole mixing problem for one coordinate,
+// Y[:, p] = W X[:, p], and it is CONTIGUOUS (N floats: 4 KiB at 1024 agents,
+// 32 KiB at 8192): every byte of X and Y streams once, sequentially, whatever
+// the graph — where the agent-major CSR kernel re-reads each row deg times
+// through L2 (47-53 % of HBM on random-regular W).
+//
+// csr_pm_kernel: one persistent 1024-thread workgroup per CU walks 32 KiB
+// stages (sr consecutive p-rows, each padded to xw floats in LDS); stages come
+// in by LDS-DMA (global_load_lds_dwordx4) into a ring of NBUF buffers with
+// NBUF - 1 stages in flight, retired by a counted s_waitcnt vmcnt and a raw
+// s_barrier (no __syncthreads(): its fence would drain the ring).  Each thread
+// owns QPT "quads" (4 consecutive output agents) for the whole kernel, with
+// their first four (column, weight) pairs in registers (columns as u16), so the
+// CSR index is read once per kernel, not once per tile; the gathers are LDS
+// reads.  Sums: +0 start, ascending CSR order, separately rounded mul and add
+// (-ffp-contract=off), entries past a row's degree skipped by a select (no
+// 0 * Inf) — bit-identical to dol_mix_csr_f32 and the reference's consensus
+// (DIST/clients.py:61-69).  Stores are buffer stores with dropped
+// out-of-range lanes, so every thread issues the same number of VMEM ops per
+// stage and the counted wait is exact.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <stdlib.h>
+
+#include <algorithm>
+#include <type_traits>
+
+#include "../../include/dol_hip.h"
+#include "dol_common.h"
+
+#define DOL_GPTR(p) ((const __attribute__((address_space(1))) void*)(p))
+#define DOL_LPTR(p) ((__attribute__((address_space(3))) void*)(p))
+
+namespace {
+using dol::check_launch;
+using dol::fail;
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+using rsrc_t = __amdgpu_buffer_rsrc_t;
+
+constexpr int kT = 1024;                  // threads per workgroup (16 waves)
+constexpr int kStageF = 8192;             // floats per stage buffer (32 KiB)
+constexpr int kDma = kStageF / 4 / kT;    // LDS-DMA instructions per thread per stage (2)
+constexpr uint32_t kOOB = 0x80000000u;    // a buffer offset past every range: the store is dropped
+
+__device__ __forceinline__ void wait_vmcnt(int n) {
+  switch (n) {
+#define DOL_VMC(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
+    DOL_VMC(1) DOL_VMC(2) DOL_VMC(3) DOL_VMC(4) DOL_VMC(5) DOL_VMC(6) DOL_VMC(7)
+    DOL_VMC(8) DOL_VMC(9) DOL_VMC(10) DOL_VMC(11) DOL_VMC(12) DOL_VMC(13) DOL_VMC(14) DOL_VMC(15)
+#undef DOL_VMC
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+__device__ __forceinline__ rsrc_t make_rsrc(const float* p, uint32_t nbytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), 0, static_cast<int>(nbytes), 0x00020000);
+}
+
+// one output quad: agents 4q .. 4q+3, their first four neighbours (u16 columns,
+// two per register), weights and degrees (4 bits each, min(degree, 15))
+struct Quad {
+  uint32_t c[4][2];
+  float w[4][4];
+  uint32_t deg;
+};
+
+__device__ __forceinline__ void load_quad(Quad& Q, int q, int n_rows, int nnz, const int32_t* __restrict__ rowptr,
+                                          const int32_t* __restrict__ col, const float* __restrict__ val) {
+  // unconditional loads from clamped addresses, all issued before any use (a
+  // predicated load compiles to a branch + vmcnt(0) per element)
+  int e0[4], d[4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    const int i = min(4 * q + a, n_rows - 1);
+    e0[a] = rowptr[i];
+    d[a] = rowptr[i + 1];
+  }
+  int cj[4][4];
+  float wj[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    d[a] = 4 * q + a < n_rows ? d[a] - e0[a] : 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int ee = min(e0[a] + e, nnz - 1);
+      cj[a][e] = col[ee];
+      wj[a][e] = val[ee];
+    }
+  }
+  Q.deg = 0;
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    Q.deg |= uint32_t(d[a] < 15 ? d[a] : 15) << (4 * a);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const bool in = e < d[a];
+      const uint32_t c = in ? static_cast<uint32_t>(cj[a][e]) : 0u;
+      if (e % 2 == 0) Q.c[a][e / 2] = c;
+      else Q.c[a][e / 2] |= c << 16;
+      Q.w[a][e] = in ? wj[a][e] : 0.0f;
+    }
+  }
+}
+
+// y[a] = sum_e w[a][e] * im[col[a][e]]  (+0 start, ascending e)
+__device__ __forceinline__ f4 mix_quad(const Quad& Q, const float* __restrict__ im, int q,
+                                       const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
+                                       const float* __restrict__ val) {
+  f4 y;
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    const int d = static_cast<int>((Q.deg >> (4 * a)) & 15u);
+    float acc = 0.0f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const uint32_t cj = (Q.c[a][e / 2] >> (16 * (e % 2))) & 0xffffu;
+      const float t = Q.w[a][e] * im[cj];
+      acc = e < d ? acc + t : acc;
+    }
+    if (d > 4) {  // a long row: the rest of its list from memory (rare; correct, not fast)
+      const int i = 4 * q + a;
+      const int e1 = rowptr[i + 1];
+      for (int e = rowptr[i] + 4; e < e1; ++e) acc = acc + val[e] * im[col[e]];
+    }
+    y[a] = acc;
+  }
+  return y;
+}
+
+// LAUX / SAUX: cache-policy bits of the LDS-DMA loads / the stores (0 default,
+// 2 nontemporal); COPY: y = x of the same agent (a copy in the same geometry,
+// the structure's own ceiling; measurement only)
+template <int NBUF, int QPT, int LAUX = 0, int SAUX = 2, bool COPY = false>
+__global__ __launch_bounds__(kT) void csr_pm_kernel(const float* __restrict__ XT, int64_t ldx, int x_rows,
+                                                    float* __restrict__ YT, int64_t ldy, int n_rows, int64_t P,
+                                                    int xw, int sr, int qp_log2, int spt, int64_t n_stages,
+                                                    const int32_t* __restrict__ rowptr,
+                                                    const int32_t* __restrict__ col,
+                                                    const float* __restrict__ val) {
+  extern __shared__ __attribute__((aligned(16))) float img[];  // NBUF x kStageF
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // thread -> (quad, p-row group): QPT == 1: QP = 2^qp_log2 quads per p-row,
+  // GR = 1024 / QP p-rows side by side; QPT == 2: quads tid and tid + 1024 of one p-row
+  const int q0 = QPT == 1 ? (tid & ((1 << qp_log2) - 1)) : tid;
+  const int g = QPT == 1 ? (tid >> qp_log2) : 0;
+  const int GR = QPT == 1 ? (kT >> qp_log2) : 1;
+  const int nq = (n_rows + 3) / 4;
+  const int nnz = rowptr[n_rows];
+  Quad Q[QPT];
+  if (nnz > 0) {
+#pragma unroll
+    for (int j = 0; j < QPT; ++j) load_quad(Q[j], q0 + j * kT, n_rows, nnz, rowptr, col, val);
+  } else {
+#pragma unroll
+    for (int j = 0; j < QPT; ++j) Q[j] = Quad{};
+  }
+
+  const int64_t G = gridDim.x;
+  const int64_t nk = blockIdx.x < n_stages ? (n_stages - blockIdx.x + G - 1) / G : 0;
+  const int xq = xw / 4;                     // 16-B pieces per p-row image
+  const int xr4 = (x_rows + 3) / 4;          // pieces holding data
+  auto issue = [&](int64_t k) {              // stage k of this workgroup -> buffer k % NBUF
+    const int64_t p0 = (blockIdx.x + k * G) * sr;
+    float* dst = img + (k % NBUF) * kStageF;
+#pragma unroll
+    for (int d = 0; d < kDma; ++d) {
+      const int pc = d * kT + tid;
+      const int pr = pc / xq, j4 = pc - pr * xq;
+      const bool ok = pr < sr && p0 + pr < P && j4 < xr4;
+      const float* src = ok ? XT + (p0 + pr) * ldx + 4 * j4 : XT;  // dead pieces re-read XT[0..3]
+      __builtin_amdgcn_global_load_lds(DOL_GPTR(src), DOL_LPTR(dst + (d * kT + wave * 64) * 4), 16, 0, LAUX);
+    }
+  };
+#pragma unroll
+  for (int k = 0; k < NBUF - 1; ++k)
+    if (k < nk) issue(k);
+  for (int64_t k = 0; k < nk; ++k) {
+    // retire stage k: younger ops are the stages issued after it and (k >= 1)
+    // the previous stage's spt stores
+    const int64_t ahead = std::min<int64_t>(nk - 1, k + NBUF - 2) - k;
+    wait_vmcnt(static_cast<int>((k >= 1 ? spt : 0) + kDma * ahead));
+    __builtin_amdgcn_s_barrier();  // every wave's share landed; buffer (k-1) % NBUF is free
+    if (k + NBUF - 1 < nk) issue(k + NBUF - 1);
+    const int64_t p0 = (blockIdx.x + k * G) * sr;
+    const float* im0 = img + (k % NBUF) * kStageF;
+    const int64_t rows_here = std::min<int64_t>(sr, P - p0);
+    const rsrc_t ry = make_rsrc(YT + p0 * ldy, static_cast<uint32_t>(rows_here * ldy * 4));
+    for (int u = 0; u < spt / QPT; ++u) {
+      const int pr = g + u * GR;
+      const bool prow_ok = pr < rows_here;
+      const float* im = im0 + (pr < sr ? pr : 0) * xw;
+#pragma unroll
+      for (int j = 0; j < QPT; ++j) {
+        const int q = q0 + j * kT;
+        const f4 y = COPY ? *reinterpret_cast<const f4*>(im + 4 * (q % (xw / 4))) : mix_quad(Q[j], im, q, rowptr, col, val);
+        const uint32_t off = static_cast<uint32_t>((pr * ldy + 4 * q) * 4);
+        if (4 * q + 3 < n_rows || q >= nq) {  // whole quad, or none (dropped)
+          const bool ok = prow_ok && q < nq;
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, y),
+                                                 ry, ok ? off : kOOB, 0, SAUX);
+        } else {  // the ragged last quad (elements named one by one: hipcc 7.2 stored
+                  // element 0 four times from a loop over y[a] here)
+          const float ye[4] = {y.x, y.y, y.z, y.w};
+          const int left = n_rows - 4 * q;  // 1..3
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ye[0]), ry, prow_ok ? off : kOOB, 0, 2);
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ye[1]), ry, prow_ok && left > 1 ? off + 4 : kOOB, 0, 2);
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ye[2]), ry, prow_ok && left > 2 ? off + 8 : kOOB, 0, 2);
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this stage's LDS reads are done before the next barrier
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// ----------------------------------------------------------------------------
+// Tiled transpose B[c][r] = A[r][c] (fp32, 64 x 64 tiles through LDS, rows
+// padded by one float against bank conflicts): converts the agent-major bank
+// to the parameter-major one and back (setup / checkpoint time, not per round).
+// ----------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void transpose_kernel(const float* __restrict__ A, int64_t lda,
+                                                        float* __restrict__ B, int64_t ldb, int64_t rows,
+                                                        int64_t cols, int64_t tiles_c) {
+  __shared__ float t[64][65];
+  const int64_t tr = blockIdx.x / tiles_c, tc = blockIdx.x % tiles_c;
+  const int lx = threadIdx.x & 63, ly = threadIdx.x >> 6;
+  const int64_t r0 = tr * 64, c0 = tc * 64;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int64_t r = r0 + ly + 4 * i, c = c0 + lx;
+    if (r < rows && c < cols) t[ly + 4 * i][lx] = A[r * lda + c];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int64_t c = c0 + ly + 4 * i, r = r0 + lx;
+    if (r < rows && c < cols) B[c * ldb + r] = t[lx][ly + 4 * i];
+  }
+}
+
+int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v && *v ? atoi(v) : dflt;
+}
+
+int n_cus() {
+  static const int n = [] {
+    int dev = 0, cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cu = 0;
+    return cu;
+  }();
+  return n;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dol_mix_csr_pm_f32(const float* XT, int64_t ldx, int32_t x_rows, float* YT, int64_t ldy, int32_t n_rows,
+                       int64_t P, const int32_t* rowptr, const int32_t* col, const float* val, hipStream_t s) {
+  const char* nm = "dol_mix_csr_pm_f32";
+  if (n_rows < 0 || x_rows < 0 || P < 0) return fail(DOL_EINVAL, "%s: negative size", nm);
+  if (n_rows == 0 || P == 0) { dol::g_err[0] = '\0'; return DOL_OK; }
+  if (!XT || !YT || !rowptr || (x_rows > 0 && (!col || !val))) return fail(DOL_EINVAL, "%s: null pointer", nm);
+  if (x_rows < 1) return fail(DOL_EINVAL, "%s: x_rows must be >= 1", nm);
+  if (x_rows > kStageF || n_rows > 2 * 4 * kT)
+    return fail(DOL_EINVAL, "%s: at most %d agents (x_rows %d, n_rows %d)", nm, kStageF, x_rows, n_rows);
+  if (ldx % 4 || ldx < (x_rows + 3) / 4 * 4 || ldy % 4 || ldy < (n_rows + 3) / 4 * 4)
+    return fail(DOL_EINVAL, "%s: ldx / ldy must be multiples of 4 covering the rounded-up agent counts", nm);
+  if ((reinterpret_cast<uintptr_t>(XT) | reinterpret_cast<uintptr_t>(YT)) & 15u)
+    return fail(DOL_EINVAL, "%s: XT and YT must be 16-B aligned", nm);
+  if (XT == YT) return fail(DOL_EINVAL, "%s: XT and YT alias (Jacobi mix needs two buffers)", nm);
+  const int xw = (x_rows + 255) / 256 * 256;
+  int sr = kStageF / xw;
+  const int nq = (n_rows + 3) / 4;
+  int qpt = 1, qp_log2 = 0, spt;
+  if (nq <= kT) {
+    while ((1 << qp_log2) < nq) ++qp_log2;
+    const int gr = kT >> qp_log2;
+    if (sr >= gr) sr = std::min(sr / gr * gr, 4 * gr);
+    spt = (sr + gr - 1) / gr;
+  } else {
+    qpt = 2;
+    sr = 1;
+    spt = 2;
+  }
+  if (int64_t(sr) * ldy * 4 >= (int64_t(1) << 31)) return fail(DOL_EINVAL, "%s: ldy too large", nm);
+  const int64_t n_stages = (P + sr - 1) / sr;
+  const int ncu = n_cus();
+  if (ncu <= 0) return fail(DOL_EINVAL, "%s: no device", nm);
+  const int64_t grid = std::min<int64_t>(ncu, n_stages);
+  const int nbuf = env_int("DOL_PM_NBUF", 4) == 3 ? 3 : 4;
+  const int var = env_int("DOL_PM_VARIANT", 0);  // measurement knobs: 1 nt DMA, 2 plain stores, 3 both, 4 copy
+  auto go = [&](auto kern, int nb) {
+    const int lds = nb * kStageF * 4;
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(grid)), dim3(kT), lds, s, XT, ldx, x_rows, YT, ldy, n_rows, P,
+                       xw, sr, qp_log2, spt, n_stages, rowptr, col, val);
+  };
+  auto pick = [&](auto qc) {
+    constexpr int Q = decltype(qc)::value;
+    if (var == 1) go(csr_pm_kernel<4, Q, 2, 2>, 4);
+    else if (var == 2) go(csr_pm_kernel<4, Q, 0, 0>, 4);
+    else if (var == 3) go(csr_pm_kernel<4, Q, 2, 0>, 4);
+    else if (var == 4) go(csr_pm_kernel<4, Q, 0, 2, true>, 4);
+    else if (nbuf == 3) go(csr_pm_kernel<3, Q>, 3);
+    else go(csr_pm_kernel<4, Q>, 4);
+  };
+  if (qpt == 1) pick(std::integral_constant<int, 1>{});
+  else pick(std::integral_constant<int, 2>{});
+  return check_launch(nm);
+}
+
+int dol_transpose_f32(const float* A, int64_t lda, float* B, int64_t ldb, int64_t rows, int64_t cols, hipStream_t s) {
+  const char* nm = "dol_transpose_f32";
+  if (rows < 0 || cols < 0) return fail(DOL_EINVAL, "%s: negative size", nm);
+  if (rows == 0 || cols == 0) { dol::g_err[0] = '\0'; return DOL_OK; }
+  if (!A || !B) return fail(DOL_EINVAL, "%s: null pointer", nm);
+  if (lda < cols || ldb < rows) return fail(DOL_EINVAL, "%s: lda < cols or ldb < rows", nm);
+  if (A == B) return fail(DOL_EINVAL, "%s: in-place transpose is not supported", nm);
+  const int64_t tr = (rows + 63) / 64, tc = (cols + 63) / 64;
+  if (tr * tc >= (int64_t(1) << 31)) return fail(DOL_EINVAL, "%s: too large", nm);
+  hipLaunchKernelGGL(transpose_kernel, dim3(static_cast<unsigned>(tr * tc)), dim3(256), 0, s, A, lda, B, ldb, rows,
+                     cols, tc);
+  return check_launch(nm);
+}
+
+}  // extern "C"

@@ -17,8 +17,11 @@ __all__ = [
     "DolNativeError", "mix_csr", "mix_ring", "mix_dense", "mix_dense_split3", "dense_split3_workspace_bytes", "split3_x_flags", "er_stochastic",
     "mix_ring_steps", "prox_admm_sgd", "admm_dual", "ordered_mean",
     "ordered_sum", "stream_copy", "dual_workspace_bytes", "prox_grad", "admm_step_dual", "mlp_step",
-    "dgd_ring", "dgd_csr", "OBJECTIVES",
+    "dgd_ring", "dgd_csr", "OBJECTIVES", "admm_ls_round", "admm_ls_round_workspace_bytes", "mix_csr_pm",
+    "transpose", "PM_MAX_AGENTS",
 ]
+
+PM_MAX_AGENTS = 8192  # dol_mix_csr_pm_f32: one p-row image (<= 32 KiB) per LDS stage
 
 
 def _stream(t: torch.Tensor) -> int:
@@ -78,6 +81,48 @@ def mix_csr(X: torch.Tensor, Y: torch.Tensor, rowptr: torch.Tensor, col: torch.T
                  rowptr.data_ptr(), col.data_ptr() if col.numel() else None,
                  val.data_ptr() if val.numel() else None, _stream(X))
     return Y
+
+
+def mix_csr_pm(XT: torch.Tensor, YT: torch.Tensor, rowptr: torch.Tensor, col: torch.Tensor, val: torch.Tensor,
+               x_agents: Optional[int] = None, P: Optional[int] = None) -> torch.Tensor:
+    """The gossip mix on the parameter-major bank: YT[p, i] = sum_e val[e] *
+    XT[p, col[e]] for every parameter row p (bit-identical to mix_csr on the
+    transposed matrices).  XT [P, >= x_agents], YT [P, >= n] (n = rowptr
+    length - 1), row strides multiples of 4, 16-B aligned; at most
+    PM_MAX_AGENTS agents.  Reference: DIST/simulators.py:91-97 +
+    DIST/clients.py:61-69."""
+    P = XT.shape[0] if P is None else P
+    n = rowptr.shape[0] - 1
+    x_agents = n if x_agents is None else int(x_agents)
+    ldx = _check_rows("XT", XT)
+    ldy = _check_rows("YT", YT)
+    if XT.shape[0] < P or YT.shape[0] < P:
+        raise ValueError(f"XT/YT need >= {P} parameter rows")
+    if XT.shape[1] < x_agents or YT.shape[1] < n:
+        raise ValueError(f"XT needs >= {x_agents} agent columns, YT >= {n}")
+    for nm, t, dt in (("rowptr", rowptr, torch.int32), ("col", col, torch.int32), ("val", val, torch.float32)):
+        if t.device != XT.device or t.dtype != dt or not t.is_contiguous():
+            raise ValueError(f"{nm}: expected contiguous {dt} on {XT.device}")
+    if XT.data_ptr() == YT.data_ptr():
+        raise ValueError("XT and YT alias: the Jacobi mix needs two buffers")
+    _native.call("dol_mix_csr_pm_f32", XT.data_ptr(), ldx, x_agents, YT.data_ptr(), ldy, n, P, rowptr.data_ptr(),
+                 col.data_ptr() if col.numel() else None, val.data_ptr() if val.numel() else None, _stream(XT))
+    return YT
+
+
+def transpose(A: torch.Tensor, B: torch.Tensor, rows: Optional[int] = None, cols: Optional[int] = None) -> torch.Tensor:
+    """B[c, r] = A[r, c] for r < rows, c < cols (tiled through LDS): converts the
+    agent-major bank [N, ld] to the parameter-major one [P, ldt] and back."""
+    rows = A.shape[0] if rows is None else rows
+    cols = A.shape[1] if cols is None else cols
+    lda = _check_rows("A", A, cols)
+    ldb = _check_rows("B", B, rows)
+    if A.shape[0] < rows or B.shape[0] < cols:
+        raise ValueError(f"shapes: A {tuple(A.shape)}, B {tuple(B.shape)}, rows {rows}, cols {cols}")
+    if A.device != B.device:
+        raise ValueError("A and B on different devices")
+    _native.call("dol_transpose_f32", A.data_ptr(), lda, B.data_ptr(), ldb, rows, cols, _stream(A))
+    return B
 
 
 def mix_ring_steps(X: torch.Tensor, Y: torch.Tensor, w_prev: torch.Tensor, w_next: torch.Tensor, steps: int,
@@ -381,6 +426,65 @@ def admm_dual(alpha: torch.Tensor, w: torch.Tensor, theta: torch.Tensor, rho: fl
             raise ValueError(f"work: need {need} bytes")
     _native.call("dol_admm_dual_f32", alpha.data_ptr(), lda, w.data_ptr(), ldw, theta.data_ptr(), float(rho),
                  n, P, _ptr(resid_sq), _ptr(work) if resid_sq is not None else None, _stream(alpha))
+
+
+def admm_ls_round_workspace_bytes(m: int, P: int) -> int:
+    return int(_native.lib().dol_admm_ls_round_workspace_bytes(int(m), int(P)))
+
+
+def admm_ls_round(w: torch.Tensor, alpha: torch.Tensor, target: torch.Tensor, theta: torch.Tensor,
+                  agents: Optional[torch.Tensor] = None, first: Optional[torch.Tensor] = None,
+                  buf: Optional[torch.Tensor] = None, rho: float = 0.1, lr: float = 0.1, momentum: float = 0.0,
+                  local_steps: int = 1, resid_sq: Optional[torch.Tensor] = None,
+                  alpha_sq: Optional[torch.Tensor] = None, work: Optional[torch.Tensor] = None,
+                  P: Optional[int] = None) -> None:
+    """One FedADMM client round on f_a(w) = 1/2 ||w - t_a||^2 for the sampled
+    rows `agents` (int32 device [m]; None = rows 0..n-1), fused per row
+    (dol_admm_ls_round_f32): w = theta, `local_steps` x (LS gradient + ADMM
+    term + momentum SGD), then the dual ascent.  first: int32 device [m],
+    nonzero where that agent's optimizer takes its first step ever.
+    resid_sq / alpha_sq: float64 [m] outputs (||w - theta||^2, ||alpha||^2).
+    Reference: DEC/clients.py:36-53, :125-144 (update_weights, update_model,
+    update_duals) with the CNN loss replaced by least squares."""
+    P = w.shape[1] if P is None else P
+    ldw = _check_rows("w", w, P)
+    lda = _check_rows("alpha", alpha, P)
+    ldt = _check_rows("target", target, P)
+    n = w.shape[0]
+    if alpha.shape[0] < n or target.shape[0] < n:
+        raise ValueError("alpha/target have fewer rows than w")
+    _check_vec("theta", theta, P, w.device)
+    if int(local_steps) < 0:
+        raise ValueError("local_steps must be >= 0")
+    ldb = 0
+    if momentum != 0.0:
+        if buf is None:
+            raise ValueError("momentum != 0 needs buf")
+        ldb = _check_rows("buf", buf, P)
+        if buf.shape[0] < n:
+            raise ValueError("buf has fewer rows than w")
+    m = n
+    if agents is not None:
+        _check_order(agents, w.device, n)
+        m = agents.numel()
+    if first is not None and (first.device != w.device or first.dtype != torch.int32 or not first.is_contiguous()
+                              or first.numel() < m):
+        raise ValueError(f"first: expected contiguous int32 [{m}] on {w.device}")
+    if (resid_sq is None) != (alpha_sq is None):
+        raise ValueError("pass both resid_sq and alpha_sq or neither")
+    if resid_sq is not None:
+        for nm, t in (("resid_sq", resid_sq), ("alpha_sq", alpha_sq)):
+            if t.dtype != torch.float64 or t.numel() < m or t.device != w.device or not t.is_contiguous():
+                raise ValueError(f"{nm}: expected contiguous float64 [{m}] on {w.device}")
+        need = admm_ls_round_workspace_bytes(m, P)
+        if work is None:
+            work = _workspace(w.device, need)
+        elif work.device != w.device or work.numel() * work.element_size() < need:
+            raise ValueError(f"work: need {need} bytes on {w.device}")
+    _native.call("dol_admm_ls_round_f32", w.data_ptr(), ldw, _ptr(buf) if ldb else None, ldb, alpha.data_ptr(), lda,
+                 target.data_ptr(), ldt, theta.data_ptr(), _ptr(agents), _ptr(first), m, P, float(rho), float(lr),
+                 float(momentum), int(local_steps), _ptr(resid_sq), _ptr(alpha_sq),
+                 _ptr(work) if resid_sq is not None else None, _stream(w))
 
 
 def _check_order(order: torch.Tensor, device, n_rows: int) -> None:

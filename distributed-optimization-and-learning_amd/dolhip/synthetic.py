@@ -79,3 +79,163 @@ class SeparableDGD:
     def consensus_error(self) -> float:
         x = self.params()
         return float((x - x.mean(0, keepdim=True)).norm() / max(1, x.shape[0]) ** 0.5)
+
+
+class SeparableADMM:
+    """FedADMM on the separable least-squares objective f_k(w) = 1/2 ||w - t_k||^2
+    over stacked agent rows (BASELINE config 4's primal/dual side).
+
+    One round is the reference's Server.run body (DEC/servers.py:50-81) with
+    the CNN loss replaced by least squares:
+      m = max(int(frac * N), 1); order = np.random.choice(range(N), m, replace=False)
+      every sampled client: FedAdmm_Client.update_weights(theta) (DEC/clients.py:36-53)
+        = w <- theta, local_steps x (update_model :125-139 + SGD.step :44), update_duals :141-144
+        -> one fused kernel over the sampled rows (dol_admm_ls_round_f32)
+      theta <- average_weights(new w in sampled order) (DEC/servers.py:42-48)
+        -> dol_ordered_mean_f32, or across ranks parallel.global_mean_exact
+           ("exact", bit-identical to one process) / parallel.global_mean
+           ("fast": local ordered sums + all_reduce(SUM), then / m).
+    The reference's server averages the primal rows only (no alpha/rho term in
+    theta, DEC/servers.py:42-48), so its iteration does NOT reach the optimum
+    mean_k t_k of sum_k f_k: with every client sampled each round, sum_k alpha_k
+    = rho*N*(theta - theta_0) holds after every round, and the fixed point
+    (w_k = theta, grad = 0 => alpha_k = t_k - theta) is
+        theta* = (mean_k t_k + rho*theta_0) / (1 + rho)          (fixed_point())
+    which the engine reproduces, bias included.
+    Each client's momentum buffer persists across rounds (the reference's
+    per-client torch.optim.SGD is never reset); its first step ever sets
+    buf = g'.  Metrics per round: sum over sampled clients of
+    ||w_k - theta||^2 (primal residual, pre-round theta) and ||alpha_k||^2.
+
+    Sharded: with torch.distributed initialised, rank r owns the contiguous
+    agent block parallel.shard_bounds(N, world, r); every rank draws the same
+    order (same seed), runs its local sampled rows, and the mean is the only
+    collective.  `round_fn` / `ordered_sum` inject CPU checkers in tests.
+    """
+
+    def __init__(self, n_agents: int, P: int, rho: float = 0.1, lr: float = 0.1, momentum: float = 0.5,
+                 local_steps: int = 1, frac: float = 1.0, seed: int = 2028, device=None, mean: str = "exact",
+                 group=None, metrics: bool = True, round_fn=None, ordered_sum=None):
+        import numpy as np
+        import torch.distributed as dist
+
+        from . import ops, parallel
+        from .bank import row_stride
+        if mean not in ("exact", "fast"):
+            raise ValueError("mean must be 'exact' or 'fast'")
+        self.N, self.P = int(n_agents), int(P)
+        self.rho, self.lr, self.mu, self.local_steps = float(rho), float(lr), float(momentum), int(local_steps)
+        self.m = max(int(frac * self.N), 1)
+        self.mean_mode, self.group, self.metrics = mean, group, metrics
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.lo, self.hi = parallel.shard_bounds(self.N, self.world, self.rank)
+        self.n = self.hi - self.lo
+        self.device = torch.device(device) if device is not None else torch.device("cuda")
+        self._round = round_fn if round_fn is not None else ops.admm_ls_round
+        self._osum = ordered_sum if ordered_sum is not None else ops.ordered_sum
+        self._parallel = parallel
+        self.rs = np.random.RandomState(seed)  # the reference's np.random.choice stream (setup_seed)
+        ld = row_stride(self.P)
+        dev = self.device
+        self.w = torch.zeros(max(self.n, 1), ld, dtype=torch.float32, device=dev)
+        self.alpha = torch.zeros_like(self.w)
+        self.target = torch.empty_like(self.w)
+        self.mom = torch.zeros_like(self.w) if self.mu != 0.0 else None
+        for k in range(self.lo, self.hi):  # per-row seeds: identical rows for every sharding
+            g = torch.Generator(device=dev).manual_seed(seed * 1000003 + k + 1)
+            self.target[k - self.lo, :self.P].normal_(generator=g)
+        g = torch.Generator(device=dev).manual_seed(seed)
+        self.theta = torch.zeros(ld, dtype=torch.float32, device=dev)
+        self.theta[:self.P].normal_(generator=g)
+        self.theta0 = self.theta.clone()
+        self._theta_next = torch.zeros_like(self.theta)
+        self.mom_started = np.zeros(max(self.n, 1), dtype=bool)
+        self.rounds = 0
+        self._pending = []  # per-round device metrics, read lazily (no sync on the round path)
+        self._history = []
+
+    def sample(self):
+        """The sampled clients of the next round, in the reference's order."""
+        return self.rs.choice(range(self.N), self.m, replace=False)
+
+    def round(self, order=None) -> None:
+        import numpy as np
+        order = np.asarray(self.sample() if order is None else order, dtype=np.int64)
+        if order.size < 1 or order.min() < 0 or order.max() >= self.N or len(set(order.tolist())) != order.size:
+            raise ValueError(f"order must be distinct agent ids in [0, {self.N})")
+        local = [int(g) - self.lo for g in order if self.lo <= g < self.hi]
+        dev = self.device
+        ml = len(local)
+        rw = ra = None
+        if ml:
+            rows = torch.as_tensor(local, dtype=torch.int32, device=dev)
+            first = None
+            if self.mom is not None:
+                first = torch.as_tensor(~self.mom_started[local], dtype=torch.int32, device=dev)
+            if self.metrics:
+                rw = torch.empty(ml, dtype=torch.float64, device=dev)
+                ra = torch.empty(ml, dtype=torch.float64, device=dev)
+            self._round(self.w, self.alpha, self.target, self.theta, agents=rows, first=first, buf=self.mom,
+                        rho=self.rho, lr=self.lr, momentum=self.mu, local_steps=self.local_steps, resid_sq=rw,
+                        alpha_sq=ra, P=self.P)
+            if self.mom is not None and self.local_steps > 0:
+                self.mom_started[local] = True
+        par = self._parallel
+        if self.mean_mode == "exact":
+            par.global_mean_exact(self.w, self.lo, self.hi, [int(g) for g in order], self.P, group=self.group,
+                                  out=self._theta_next, ordered_sum=self._osum)
+        else:
+            par.global_mean(self.w, local, self.m, self.P, group=self.group, out=self._theta_next,
+                            ordered_sum=self._osum)
+        self.theta, self._theta_next = self._theta_next, self.theta
+        if self.metrics:
+            s = torch.zeros(2, dtype=torch.float64, device=dev)
+            if ml:
+                s[0] = rw.sum()
+                s[1] = ra.sum()
+            if self.world > 1:
+                import torch.distributed as dist
+                if s.device.type == "cuda" and dist.get_backend(self.group) == "gloo":
+                    h = s.cpu()
+                    dist.all_reduce(h, group=self.group)
+                    s.copy_(h)
+                else:
+                    dist.all_reduce(s, group=self.group)
+            self._pending.append((self.rounds, s))
+        self.rounds += 1
+
+    @property
+    def history(self):
+        """Per-round metrics: {"round", "primal_resid_sq", "dual_sq"} (sums over the sampled clients)."""
+        for r, s in self._pending:
+            v = s.cpu().tolist()
+            self._history.append({"round": r, "primal_resid_sq": v[0], "dual_sq": v[1]})
+        self._pending = []
+        return self._history
+
+    def optimum(self) -> torch.Tensor:
+        """mean_k t_k in fp64 (the minimiser of sum_k f_k); all ranks (diagnostic)."""
+        s = self.target[:self.n, :self.P].double().sum(0)
+        if self.world > 1:
+            import torch.distributed as dist
+            if s.device.type == "cuda" and dist.get_backend(self.group) == "gloo":
+                h = s.cpu()
+                dist.all_reduce(h, group=self.group)
+                s.copy_(h)
+            else:
+                dist.all_reduce(s, group=self.group)
+        return s / self.N
+
+    def distance_to_optimum(self) -> float:
+        """||theta - mean_k t_k|| / sqrt(P)."""
+        return float((self.theta[:self.P].double() - self.optimum()).norm() / self.P ** 0.5)
+
+    def fixed_point(self) -> torch.Tensor:
+        """theta* = (mean_k t_k + rho*theta_0) / (1 + rho): where the reference's
+        iteration settles under full participation (see the class docstring)."""
+        return (self.optimum() + self.rho * self.theta0[:self.P].double()) / (1.0 + self.rho)
+
+    def distance_to_fixed_point(self) -> float:
+        """||theta - theta*|| / sqrt(P) (full participation)."""
+        return float((self.theta[:self.P].double() - self.fixed_point()).norm() / self.P ** 0.5)

@@ -59,6 +59,29 @@ int dol_mix_csr_f32(const float* X, int64_t ldx, int32_t x_rows,
                     hipStream_t s);
 
 /*
+ * dol_mix_csr_f32 on the PARAMETER-MAJOR bank (the agent-major one
+ * transposed): XT[p * ldx + j] = agent j's parameter p, for p < P.
+ *   YT[p][i] = sum_{e in rowptr[i]..rowptr[i+1]} val[e] * XT[p][col[e]]
+ * Same reference code and the same rounding as dol_mix_csr_f32 (bit-identical
+ * results, transposed): DIST/simulators.py:91-97 + DIST/clients.py:61-69.
+ * Each p-row is one contiguous mixing problem, so X and Y stream from HBM once
+ * in order for any graph (the agent-major CSR kernel re-reads each row deg
+ * times).  Limits: x_rows, n_rows <= 8192; ldx, ldy multiples of 4 with
+ * ldx >= round_up(x_rows, 4), ldy >= round_up(n_rows, 4); XT, YT 16-B aligned,
+ * not aliased; 0 <= col < x_rows.
+ */
+int dol_mix_csr_pm_f32(const float* XT, int64_t ldx, int32_t x_rows, float* YT, int64_t ldy, int32_t n_rows,
+                       int64_t P, const int32_t* rowptr, const int32_t* col, const float* val, hipStream_t s);
+
+/*
+ * B[c * ldb + r] = A[r * lda + c] for r < rows, c < cols (fp32, tiled through
+ * LDS): converts the agent-major bank to the parameter-major one and back
+ * (setup and checkpoint time, not on the round path).  A and B must not alias.
+ */
+int dol_transpose_f32(const float* A, int64_t lda, float* B, int64_t ldb, int64_t rows, int64_t cols,
+                      hipStream_t s);
+
+/*
  * Ring (circle topology) specialisation of dol_mix_csr_f32:
  *   Y[i,:] = fl(fl(+0 + fl(w_prev[i]*X[i-1,:])) + fl(w_next[i]*X[i+1,:]))
  * Replaces the same reference code as dol_mix_csr_f32 for

@@ -53,6 +53,10 @@ def lib():
         L.oracle_dgd_local_f32.argtypes = [_f32p, _i64, _f32p, _i64, _f32p, _i64, _i32, _i64, _i32, _i32,
                                            ctypes.c_float, ctypes.c_float, ctypes.c_int]
         L.oracle_dgd_local_f32.restype = None
+        L.oracle_admm_ls_round_f32.argtypes = [_f32p, _i64, _f32p, _i64, _f32p, _i64, _f32p, _i64, _f32p, _i32p, _i32p,
+                                               _i32, _i64, ctypes.c_float, ctypes.c_float, ctypes.c_float, _i32,
+                                               _f64p, _f64p]
+        L.oracle_admm_ls_round_f32.restype = None
         for f in (L.oracle_mix_csr_f32, L.oracle_mix_ring_f32, L.oracle_prox_admm_sgd_f32,
                   L.oracle_admm_dual_f32, L.oracle_ordered_mean_f32, L.oracle_ordered_sum_f32):
             f.restype = None
@@ -154,6 +158,25 @@ def dgd_local(Y, T, M, objective, steps, lr, momentum, first_step):
     lib().oracle_dgd_local_f32(_p(Y), P, _p(T), P, _p(M), P, n, P, OBJECTIVES[objective], int(steps), lr,
                                momentum, int(first_step))
     return Y, M
+
+
+def admm_ls_round(w, buf, alpha, target, theta, agents, first, rho, lr, momentum, local_steps):
+    """One FedADMM least-squares client round for the sampled rows `agents`
+    (config 4); returns (w', buf', alpha', resid_sq[m], alpha_sq[m]) on copies."""
+    w = _f32c(w).copy()
+    alpha = _f32c(alpha).copy()
+    n, P = w.shape
+    buf = None if buf is None else _f32c(buf).copy()
+    T = _f32c(target)
+    ag = np.ascontiguousarray(agents, np.int32)
+    m = len(ag)
+    fs = None if first is None else np.ascontiguousarray(first, np.int32)
+    rw = np.zeros(m, np.float64)
+    ra = np.zeros(m, np.float64)
+    lib().oracle_admm_ls_round_f32(_p(w), P, _p(buf), P, _p(alpha), P, _p(T), P, _p(_f32c(theta)), _p(ag, _i32p),
+                                   _p(fs, _i32p), m, P, rho, lr, momentum, int(local_steps), _p(rw, _f64p),
+                                   _p(ra, _f64p))
+    return w, buf, alpha, rw, ra
 
 
 def bits_equal(a, b):

@@ -1,0 +1,111 @@
+"""FedADMM on least squares (BASELINE config 4's primal/dual side) on the GPU:
+dol_admm_ls_round_f32 + the ordered mean through dolhip.synthetic.SeparableADMM.
+
+* Replays the REFERENCE's own FedAdmm_Server.run on a least-squares model
+  (tests/golden/admm_ls.npz, made by tests/golden/make_golden_admm.py) bit for
+  bit: every round's theta, the final w / momentum / alpha rows.
+* Matches the oracle bit for bit at ragged and unaligned sizes (vector and
+  scalar paths), with the fp64 residual outputs within rtol 1e-12 (their
+  reduction order differs from the oracle's sequential sum).
+* Converges to the reference iteration's closed-form fixed point."""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from oracle import bits_equal
+from conftest import golden
+from dolhip import ops
+from dolhip.synthetic import SeparableADMM
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("case", ["mini_mom", "flat_nomom", "mini_full"])
+def test_admm_ls_replays_reference_server(case, gpu):
+    g = golden("admm_ls")
+    N, frac, rounds, steps, lr, mom, rho = g[f"{case}__params"]
+    N, rounds, steps = int(N), int(rounds), int(steps)
+    T = g[f"{case}__targets"]
+    P = T.shape[1]
+    s = SeparableADMM(N, P, rho=rho, lr=lr, momentum=mom, local_steps=steps, frac=frac, device=gpu)
+    s.target[:, :P] = torch.as_tensor(T, device=gpu)
+    s.theta[:P] = torch.as_tensor(g[f"{case}__theta0"], device=gpu)
+    sampled = np.zeros(N, bool)
+    for r in range(rounds):
+        order = g[f"{case}__orders"][r]
+        s.round(order=order)
+        sampled[order] = True
+        assert bits_equal(s.theta[:P].cpu().numpy(), g[f"{case}__thetas"][r]), f"round {r}"
+    assert bits_equal(s.w[:N, :P].cpu().numpy()[sampled], g[f"{case}__w"][sampled])
+    assert bits_equal(s.alpha[:N, :P].cpu().numpy(), g[f"{case}__alpha"])
+    if mom != 0:
+        assert bits_equal(s.mom[:N, :P].cpu().numpy(), g[f"{case}__mom"])
+    assert len(s.history) == rounds
+
+
+@pytest.mark.parametrize("P,extra", [(4096, 0), (1031, 0), (1031, 1), (3, 0), (5000, 3)])
+@pytest.mark.parametrize("mom,steps", [(0.5, 3), (0.0, 1), (0.9, 0)])
+def test_admm_ls_round_vs_oracle(P, extra, mom, steps, gpu):
+    rng = np.random.default_rng(P + steps)
+    N, m = 9, 5
+    ld = P + extra  # extra = 1 / 3: rows not 16-B aligned -> the scalar path
+
+    def mat(a):
+        t = torch.full((N, ld), float("nan"), device=gpu)
+        t[:, :P] = torch.as_tensor(a, device=gpu)
+        return t
+    T = rng.standard_normal((N, P)).astype(np.float32)
+    A = (0.1 * rng.standard_normal((N, P))).astype(np.float32)
+    B = rng.standard_normal((N, P)).astype(np.float32)
+    th = rng.standard_normal(P).astype(np.float32)
+    T[1, :3] = [np.inf, -0.0, 1e-40]
+    order = np.array([7, 2, 0, 8, 5], np.int32)
+    first = np.array([1, 0, 1, 0, 0], np.int32)
+    w, a, b, t = mat(np.zeros((N, P), np.float32)), mat(A), mat(B), mat(T)
+    rw = torch.empty(m, dtype=torch.float64, device=gpu)
+    ra = torch.empty(m, dtype=torch.float64, device=gpu)
+    ops.admm_ls_round(w, a, t, torch.as_tensor(th, device=gpu), agents=torch.as_tensor(order, device=gpu),
+                      first=torch.as_tensor(first, device=gpu), buf=b if mom else None, rho=0.1, lr=0.05,
+                      momentum=mom, local_steps=steps, resid_sq=rw, alpha_sq=ra, P=P)
+    torch.cuda.synchronize()
+    w1, b1, a1, rw1, ra1 = oracle.admm_ls_round(np.zeros((N, P), np.float32), B if mom else None, A, T, th, order,
+                                                first, 0.1, 0.05, mom, steps)
+    assert bits_equal(w.cpu().numpy()[order][:, :P], w1[order])
+    assert bits_equal(a.cpu().numpy()[:, :P], a1)
+    if mom:
+        assert bits_equal(b.cpu().numpy()[:, :P], b1)
+    np.testing.assert_allclose(rw.cpu().numpy(), rw1, rtol=1e-12)
+    fin = np.isfinite(ra1)
+    np.testing.assert_allclose(ra.cpu().numpy()[fin], ra1[fin], rtol=1e-12)
+
+
+def test_separable_admm_converges_to_reference_fixed_point(gpu):
+    s = SeparableADMM(64, 10000, rho=0.1, lr=0.2, momentum=0.5, local_steps=2, frac=1.0, device=gpu, seed=4)
+    for _ in range(80):
+        s.round()
+    assert s.distance_to_fixed_point() < 1e-5
+    h = s.history
+    assert h[-1]["primal_resid_sq"] < 1e-3 * h[0]["primal_resid_sq"]
+
+
+def test_separable_admm_fast_mean_close_to_exact(gpu):
+    """The all-reduce-shaped 'fast' mean (one process: the same ordered sum) is
+    bit-identical to the exact one at world size 1."""
+    a = SeparableADMM(20, 777, frac=0.5, device=gpu, seed=2, mean="exact")
+    b = SeparableADMM(20, 777, frac=0.5, device=gpu, seed=2, mean="fast")
+    for _ in range(4):
+        a.round()
+        b.round()
+    assert bits_equal(a.theta.cpu().numpy(), b.theta.cpu().numpy())
+
+
+def test_admm_ls_round_argument_errors(gpu):
+    w = torch.zeros(4, 8, device=gpu)
+    th = torch.zeros(8, device=gpu)
+    with pytest.raises(ValueError, match="buf"):
+        ops.admm_ls_round(w, w.clone(), w.clone(), th, momentum=0.5)
+    with pytest.raises(ValueError, match="both"):
+        ops.admm_ls_round(w, w.clone(), w.clone(), th, resid_sq=torch.zeros(4, dtype=torch.float64, device=gpu))
+    with pytest.raises(ValueError, match="first"):
+        ops.admm_ls_round(w, w.clone(), w.clone(), th, first=torch.zeros(2, dtype=torch.int32, device=gpu))

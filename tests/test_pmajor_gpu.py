@@ -1,0 +1,158 @@
+"""The parameter-major (transposed) bank: dol_mix_csr_pm_f32 and
+dol_transpose_f32 through the C-ABI.  The mix is bit-exact against the
+reference's own consensus vectors (tests/golden/mix.npz, transposed) and
+against the oracle on random-regular, long-row, empty-row, rectangular and
+non-finite inputs, at ragged agent counts up to the 8192 limit, and on sampled
+parameter rows at BASELINE config 3's full 1024 x 2^20."""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from oracle import bits_equal
+from conftest import golden
+from dolhip import graph as G
+from dolhip import ops
+
+pytestmark = pytest.mark.gpu
+
+
+def csr_dev(c, gpu):
+    return (torch.as_tensor(np.asarray(c.rowptr, np.int32), device=gpu),
+            torch.as_tensor(np.asarray(c.col, np.int32), device=gpu),
+            torch.as_tensor(np.asarray(c.val, np.float32), device=gpu))
+
+
+def pm(X, gpu, extra=0):
+    """Parameter-major device copy of agent-major X [n, P]: [P, round_up(n, 4) + extra], NaN padding."""
+    n, P = X.shape
+    ld = (n + 3) // 4 * 4 + extra
+    t = torch.full((P, ld), float("nan"), dtype=torch.float32, device=gpu)
+    t[:, :n] = torch.as_tensor(np.ascontiguousarray(X.T), device=gpu)
+    return t
+
+
+def run_pm(X, c, gpu, x_agents=None, extra=0):
+    rp, col, val = csr_dev(c, gpu)
+    XT = pm(X, gpu, extra)
+    n = len(c.rowptr) - 1
+    YT = torch.full((X.shape[1], (n + 3) // 4 * 4 + extra), 7.0, device=gpu)
+    ops.mix_csr_pm(XT, YT, rp, col, val, x_agents=x_agents if x_agents is not None else X.shape[0])
+    torch.cuda.synchronize()
+    out = YT.cpu().numpy()
+    assert (out[:, n:] == 7.0).all(), "wrote past the last agent"
+    return np.ascontiguousarray(out[:, :n].T)
+
+
+def _mix_cases():
+    return sorted(k[:-3] for k in golden("mix").files if k.endswith("__X"))
+
+
+@pytest.mark.parametrize("case", _mix_cases())
+def test_pm_mix_matches_reference_consensus(case, gpu):
+    mix, csr = golden("mix"), golden("csr")
+    gkey, _l, t = case.split("__")
+    k = f"{gkey}__{t}"
+    n = len(csr[k + "__rowptr"]) - 1
+    c = G.CSR(n, n, csr[k + "__rowptr"], csr[k + "__col"], csr[k + "__val"])
+    assert bits_equal(run_pm(mix[case + "__X"], c, gpu), mix[case + "__Y"])
+
+
+@pytest.mark.parametrize("n", [5, 64, 100, 257, 1000, 1024, 1025, 2047, 4096, 5000, 8192])
+@pytest.mark.parametrize("P", [1, 7, 300])
+def test_pm_mix_random_regular_vs_oracle(n, P, gpu):
+    c = G.random_regular_csr(n, 4, seed=n + 3)
+    X = np.random.default_rng(n * 7 + P).standard_normal((n, P)).astype(np.float32)
+    assert bits_equal(run_pm(X, c, gpu, extra=4 * (n % 3)), oracle.mix_csr(X, c.rowptr, c.col, c.val))
+
+
+@pytest.mark.parametrize("nbuf", ["3", "4"])
+def test_pm_mix_ring_depths_bit_identical(nbuf, gpu, monkeypatch):
+    monkeypatch.setenv("DOL_PM_NBUF", nbuf)
+    torch.manual_seed(2028)
+    c = G.communication_csr("circle", "stochastic", 1000)[0]
+    X = np.random.default_rng(1).standard_normal((1000, 2500)).astype(np.float32)
+    assert bits_equal(run_pm(X, c, gpu), oracle.mix_csr(X, c.rowptr, c.col, c.val))
+
+
+def test_pm_mix_long_empty_rectangular_and_nonfinite(gpu):
+    rng = np.random.default_rng(5)
+    # long rows: the complete graph (degree n - 1) and a dense-ish Erdos-Renyi
+    torch.manual_seed(2028)
+    W = G.communication_graph("compelete", "stochastic", 40)[0]
+    c = G.csr_from_dense(W)
+    X = rng.standard_normal((40, 333)).astype(np.float32)
+    X[3, 7], X[9, 8], X[11, 9], X[12, 10] = np.inf, np.nan, -0.0, 1e-40
+    assert bits_equal(run_pm(X, c, gpu), oracle.mix_csr(X, c.rowptr, c.col, c.val))
+    # empty rows (the dynamic topology: one edge per step) and Inf/NaN next to
+    # skipped register slots (no 0 * Inf)
+    torch.manual_seed(2028)
+    for Wt in G.communication_graph("dynamic", "stochastic", 9)[:3]:
+        c = G.csr_from_dense(Wt)
+        X = rng.standard_normal((9, 50)).astype(np.float32)
+        X[0, :5] = np.inf
+        X[1, 5:9] = np.nan
+        assert bits_equal(run_pm(X, c, gpu), oracle.mix_csr(X, c.rowptr, c.col, c.val))
+    # rectangular: 50 output agents gathering from 70 input agents, mixed degrees
+    rowptr, col, val = [0], [], []
+    for i in range(50):
+        d = int(rng.integers(0, 9))
+        cols = np.sort(rng.choice(70, d, replace=False))
+        col += cols.tolist()
+        val += rng.random(d).astype(np.float32).tolist()
+        rowptr.append(len(col))
+    c = G.CSR(50, 70, np.array(rowptr, np.int32), np.array(col, np.int32), np.array(val, np.float32))
+    X = rng.standard_normal((70, 123)).astype(np.float32)
+    want = oracle.mix_csr(X, c.rowptr, c.col, c.val)
+    assert bits_equal(run_pm(X, c, gpu), want)
+
+
+def test_pm_mix_full_size_sampled_rows(gpu):
+    """BASELINE config 3 at full size, 1024 agents x 2^20 on a random 4-regular
+    W: 64 sampled parameter rows (and the last one) bit-exact vs the oracle,
+    plus the column-sum identity sum_i YT[p][i] = sum_j colsum(W)_j XT[p][j]
+    (fp64, rtol 1e-5) on every row."""
+    n, P = 1024, 1 << 20
+    c = G.random_regular_csr(n, 4, seed=2028)
+    rp, col, val = csr_dev(c, gpu)
+    g = torch.Generator(device=gpu).manual_seed(9)
+    XT = torch.empty(P, n, device=gpu).normal_(generator=g)
+    YT = torch.empty_like(XT)
+    ops.mix_csr_pm(XT, YT, rp, col, val)
+    torch.cuda.synchronize()
+    rows = np.concatenate([np.random.default_rng(3).choice(P, 64, replace=False), [P - 1]])
+    Xs = XT[torch.as_tensor(rows, device=gpu)].cpu().numpy()
+    want = oracle.mix_csr(np.ascontiguousarray(Xs.T), c.rowptr, c.col, c.val)
+    got = YT[torch.as_tensor(rows, device=gpu)].cpu().numpy().T
+    assert bits_equal(got, want)
+    colsum = np.zeros(n, np.float64)
+    np.add.at(colsum, c.col, c.val.astype(np.float64))
+    lhs = YT.double().sum(1)
+    rhs = XT.double() @ torch.as_tensor(colsum, device=gpu)
+    torch.testing.assert_close(lhs, rhs, rtol=1e-5, atol=1e-6 * float(rhs.abs().max()))
+
+
+@pytest.mark.parametrize("rows,cols", [(1, 1), (5, 300), (1024, 4099), (333, 64), (70, 1)])
+def test_transpose_roundtrip(rows, cols, gpu):
+    A = torch.randn(rows, cols + 3, device=gpu)
+    B = torch.full((cols, rows + 5), 9.0, device=gpu)
+    ops.transpose(A, B, rows, cols)
+    C = torch.full((rows, cols + 3), 4.0, device=gpu)
+    ops.transpose(B, C, cols, rows)
+    torch.cuda.synchronize()
+    assert torch.equal(B[:, :rows], A[:, :cols].T)
+    assert (B[:, rows:] == 9.0).all()
+    assert torch.equal(C[:, :cols], A[:, :cols])
+
+
+def test_pm_mix_argument_errors(gpu):
+    c = G.random_regular_csr(16, 4, seed=1)
+    rp, col, val = csr_dev(c, gpu)
+    XT = torch.zeros(10, 16, device=gpu)
+    with pytest.raises(ops.DolNativeError, match="at most"):
+        ops.mix_csr_pm(torch.zeros(2, 8196, device=gpu), torch.zeros(2, 8196, device=gpu), rp, col, val,
+                       x_agents=8193)
+    with pytest.raises(ops.DolNativeError, match="multiples of 4"):
+        ops.mix_csr_pm(torch.zeros(10, 18, device=gpu)[:, :17], torch.zeros(10, 16, device=gpu), rp, col, val)
+    with pytest.raises(ValueError, match="alias"):
+        ops.mix_csr_pm(XT, XT, rp, col, val)

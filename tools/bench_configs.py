@@ -146,6 +146,37 @@ def dgd_round(N, P, topo, objective, momentum, steps, reps, dev):
     torch.cuda.empty_cache()
 
 
+def pm_round(N, P, topo, reps, dev, X, Y):
+    """One X <- W X round on the parameter-major bank (XT[p][j], p-row stride
+    round_up(N, 4)), reusing X / Y's memory as XT / YT."""
+    from dolhip import ops
+    if topo == "ring":
+        torch.manual_seed(2028)
+        c = G.communication_csr("circle", "stochastic", N)[0]
+    else:
+        c = G.random_regular_csr(N, int(topo[2:]), seed=2028)
+    ld = (N + 3) // 4 * 4
+    XT = X.view(-1)[: P * ld].view(P, ld)
+    YT = Y.view(-1)[: P * ld].view(P, ld)
+    rp = torch.as_tensor(c.rowptr, dtype=torch.int32, device=dev)
+    col = torch.as_tensor(c.col, dtype=torch.int32, device=dev)
+    val = torch.as_tensor(c.val, dtype=torch.float32, device=dev)
+    for _ in range(2):
+        ops.mix_csr_pm(XT, YT, rp, col, val)
+    torch.cuda.synchronize()
+    s_, e_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s_.record()
+    for _ in range(reps):
+        ops.mix_csr_pm(XT, YT, rp, col, val)
+    e_.record()
+    torch.cuda.synchronize()
+    ms = s_.elapsed_time(e_) / reps
+    alg = 2 * N * P * 4
+    print(json.dumps({"topology": topo + "-pm", "kernel": "csr_pm (parameter-major bank)", "agents": N, "params": P,
+                      "nnz": int(c.nnz), "ms_per_launch": ms, "rounds_per_s": 1e3 / ms,
+                      "GBps": alg / (ms / 1e3) / 1e9, "frac_of_8TBps": alg / (ms / 1e3) / 1e9 / 8000.0}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--agents", type=int, nargs="*", default=[1024, 8192])
@@ -170,6 +201,9 @@ def main():
         X = torch.empty(N, ld, device=dev).normal_()
         Y = torch.empty_like(X)
         for topo in a.topologies:
+            if topo.endswith("-pm"):  # the parameter-major bank: XT [P, N] (dol_mix_csr_pm_f32)
+                pm_round(N, P, topo[:-3], a.reps, dev, X, Y)
+                continue
             t0 = time.time()
             steps = 1
             extra = {}
