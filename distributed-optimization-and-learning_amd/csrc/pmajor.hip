@@ -48,9 +48,8 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u4 __attribute__((ext_vector_type(4)));
 using rsrc_t = __amdgpu_buffer_rsrc_t;
 
-constexpr int kT = 1024;                  // threads per workgroup (16 waves)
-constexpr int kStageF = 8192;             // floats per stage buffer (32 KiB)
-constexpr int kDma = kStageF / 4 / kT;    // LDS-DMA instructions per thread per stage (2)
+constexpr int kMaxAgents = 8192;          // one p-row image fits a 32 KiB stage
+constexpr int kT1 = 1024;                 // threads per workgroup (16 waves, one workgroup per CU)
 constexpr uint32_t kOOB = 0x80000000u;    // a buffer offset past every range: the store is dropped
 
 __device__ __forceinline__ void wait_vmcnt(int n) {
@@ -138,49 +137,94 @@ __device__ __forceinline__ f4 mix_quad(const Quad& Q, const float* __restrict__ 
   return y;
 }
 
-// LAUX / SAUX: cache-policy bits of the LDS-DMA loads / the stores (0 default,
-// 2 nontemporal); COPY: y = x of the same agent (a copy in the same geometry,
-// the structure's own ceiling; measurement only)
-template <int NBUF, int QPT, int LAUX = 0, int SAUX = 2, bool COPY = false>
-__global__ __launch_bounds__(kT) void csr_pm_kernel(const float* __restrict__ XT, int64_t ldx, int x_rows,
-                                                    float* __restrict__ YT, int64_t ldy, int n_rows, int64_t P,
-                                                    int xw, int sr, int qp_log2, int spt, int64_t n_stages,
-                                                    const int32_t* __restrict__ rowptr,
-                                                    const int32_t* __restrict__ col,
-                                                    const float* __restrict__ val) {
-  extern __shared__ __attribute__((aligned(16))) float img[];  // NBUF x kStageF
+// Mix one stage image (sr p-rows of xw floats at im0, p-rows p0 ..) and store
+// its rows of YT: spt buffer stores per thread, out-of-range ones dropped.
+template <int T, int QPT, int SAUX, bool COPY>
+__device__ __forceinline__ void mix_stage(const Quad (&Q)[QPT], const float* __restrict__ im0, float* __restrict__ YT,
+                                          int64_t ldy, int n_rows, int64_t P, int64_t p0, int xw, int sr, int spt,
+                                          int q0, int g, int GR, const int32_t* __restrict__ rowptr,
+                                          const int32_t* __restrict__ col, const float* __restrict__ val) {
+  const int nq = (n_rows + 3) / 4;
+  const int xq = xw / 4;
+  const int64_t rows_here = std::min<int64_t>(sr, P - p0);
+  const rsrc_t ry = make_rsrc(YT + p0 * ldy, static_cast<uint32_t>(rows_here * ldy * 4));
+  for (int u = 0; u < spt / QPT; ++u) {
+    const int pr = g + u * GR;
+    const bool prow_ok = pr < rows_here;
+    const float* im = im0 + (pr < sr ? pr : 0) * xw;
+#pragma unroll
+    for (int j = 0; j < QPT; ++j) {
+      const int q = q0 + j * T;
+      const f4 y = COPY ? *reinterpret_cast<const f4*>(im + 4 * (q % xq)) : mix_quad(Q[j], im, q, rowptr, col, val);
+      const uint32_t off = static_cast<uint32_t>((pr * ldy + 4 * q) * 4);
+      if (4 * q + 3 < n_rows || q >= nq) {  // whole quad, or none (dropped)
+        const bool ok = prow_ok && q < nq;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, y), ry, ok ? off : kOOB, 0, SAUX);
+      } else {  // the ragged last quad (elements named one by one: hipcc 7.2 stored
+                // element 0 four times from a loop over y[a] here)
+        const float ye[4] = {y.x, y.y, y.z, y.w};
+        const int left = n_rows - 4 * q;  // 1..3
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ye[0]), ry, prow_ok ? off : kOOB, 0, SAUX);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ye[1]), ry, prow_ok && left > 1 ? off + 4 : kOOB, 0,
+                                              SAUX);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ye[2]), ry, prow_ok && left > 2 ? off + 8 : kOOB, 0,
+                                              SAUX);
+      }
+    }
+  }
+}
+
+// T threads per workgroup, SF floats per stage buffer, NBUF buffers, QPT
+// quads per thread.  LAUX / SAUX: cache-policy bits of the LDS-DMA loads / the
+// stores (0 default, 2 nontemporal); COPY: y = x of the same agent (a copy in
+// the same geometry: the structure's own ceiling, measurement only).
+template <int T, int SF, int NBUF, int QPT, int LAUX, int SAUX, bool COPY = false>
+__global__ __launch_bounds__(T) void csr_pm_kernel(const float* __restrict__ XT, int64_t ldx, int x_rows,
+                                                   float* __restrict__ YT, int64_t ldy, int n_rows, int64_t P,
+                                                   int xw, int sr, int qp_log2, int spt, int64_t n_stages, int nseg,
+                                                   const int32_t* __restrict__ rowptr,
+                                                   const int32_t* __restrict__ col,
+                                                   const float* __restrict__ val) {
+  constexpr int kDma = SF / 4 / T;  // LDS-DMA instructions per thread per stage
+  static_assert(kDma * 4 * T == SF, "a stage is a whole number of DMA rounds");
+  extern __shared__ __attribute__((aligned(16))) float img[];  // NBUF x SF
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   // thread -> (quad, p-row group): QPT == 1: QP = 2^qp_log2 quads per p-row,
-  // GR = 1024 / QP p-rows side by side; QPT == 2: quads tid and tid + 1024 of one p-row
+  // GR = T / QP p-rows side by side; QPT > 1: quads tid + j*T of one p-row
   const int q0 = QPT == 1 ? (tid & ((1 << qp_log2) - 1)) : tid;
   const int g = QPT == 1 ? (tid >> qp_log2) : 0;
-  const int GR = QPT == 1 ? (kT >> qp_log2) : 1;
-  const int nq = (n_rows + 3) / 4;
+  const int GR = QPT == 1 ? (T >> qp_log2) : 1;
   const int nnz = rowptr[n_rows];
   Quad Q[QPT];
   if (nnz > 0) {
 #pragma unroll
-    for (int j = 0; j < QPT; ++j) load_quad(Q[j], q0 + j * kT, n_rows, nnz, rowptr, col, val);
+    for (int j = 0; j < QPT; ++j) load_quad(Q[j], q0 + j * T, n_rows, nnz, rowptr, col, val);
   } else {
 #pragma unroll
     for (int j = 0; j < QPT; ++j) Q[j] = Quad{};
   }
 
-  const int64_t G = gridDim.x;
-  const int64_t nk = blockIdx.x < n_stages ? (n_stages - blockIdx.x + G - 1) / G : 0;
-  const int xq = xw / 4;                     // 16-B pieces per p-row image
-  const int xr4 = (x_rows + 3) / 4;          // pieces holding data
-  auto issue = [&](int64_t k) {              // stage k of this workgroup -> buffer k % NBUF
-    const int64_t p0 = (blockIdx.x + k * G) * sr;
-    float* dst = img + (k % NBUF) * kStageF;
+  // stage order: the P range is cut into nseg contiguous segments; workgroup b
+  // walks segment b % nseg with stride gridDim / nseg, so the chip streams
+  // nseg separate regions at once (nseg = 8: +4-5 % over one sweep)
+  const int64_t W = gridDim.x / nseg, seg = blockIdx.x % nseg, wl = blockIdx.x / nseg;
+  const int64_t seg_len = (n_stages + nseg - 1) / nseg;
+  const int64_t seg_n = std::max<int64_t>(0, std::min<int64_t>(seg_len, n_stages - seg * seg_len));
+  const int64_t nk = wl < seg_n ? (seg_n - wl + W - 1) / W : 0;
+  auto stage_of = [&](int64_t k) { return seg * seg_len + wl + k * W; };
+  const int xq = xw / 4;             // 16-B pieces per p-row image
+  const int xr4 = (x_rows + 3) / 4;  // pieces holding data
+  auto issue = [&](int64_t k) {      // stage k of this workgroup -> buffer k % NBUF
+    const int64_t p0 = stage_of(k) * sr;
+    float* dst = img + (k % NBUF) * SF;
 #pragma unroll
     for (int d = 0; d < kDma; ++d) {
-      const int pc = d * kT + tid;
+      const int pc = d * T + tid;
       const int pr = pc / xq, j4 = pc - pr * xq;
       const bool ok = pr < sr && p0 + pr < P && j4 < xr4;
       const float* src = ok ? XT + (p0 + pr) * ldx + 4 * j4 : XT;  // dead pieces re-read XT[0..3]
-      __builtin_amdgcn_global_load_lds(DOL_GPTR(src), DOL_LPTR(dst + (d * kT + wave * 64) * 4), 16, 0, LAUX);
+      __builtin_amdgcn_global_load_lds(DOL_GPTR(src), DOL_LPTR(dst + (d * T + wave * 64) * 4), 16, 0, LAUX);
     }
   };
 #pragma unroll
@@ -193,33 +237,9 @@ __global__ __launch_bounds__(kT) void csr_pm_kernel(const float* __restrict__ XT
     wait_vmcnt(static_cast<int>((k >= 1 ? spt : 0) + kDma * ahead));
     __builtin_amdgcn_s_barrier();  // every wave's share landed; buffer (k-1) % NBUF is free
     if (k + NBUF - 1 < nk) issue(k + NBUF - 1);
-    const int64_t p0 = (blockIdx.x + k * G) * sr;
-    const float* im0 = img + (k % NBUF) * kStageF;
-    const int64_t rows_here = std::min<int64_t>(sr, P - p0);
-    const rsrc_t ry = make_rsrc(YT + p0 * ldy, static_cast<uint32_t>(rows_here * ldy * 4));
-    for (int u = 0; u < spt / QPT; ++u) {
-      const int pr = g + u * GR;
-      const bool prow_ok = pr < rows_here;
-      const float* im = im0 + (pr < sr ? pr : 0) * xw;
-#pragma unroll
-      for (int j = 0; j < QPT; ++j) {
-        const int q = q0 + j * kT;
-        const f4 y = COPY ? *reinterpret_cast<const f4*>(im + 4 * (q % (xw / 4))) : mix_quad(Q[j], im, q, rowptr, col, val);
-        const uint32_t off = static_cast<uint32_t>((pr * ldy + 4 * q) * 4);
-        if (4 * q + 3 < n_rows || q >= nq) {  // whole quad, or none (dropped)
-          const bool ok = prow_ok && q < nq;
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, y),
-                                                 ry, ok ? off : kOOB, 0, SAUX);
-        } else {  // the ragged last quad (elements named one by one: hipcc 7.2 stored
-                  // element 0 four times from a loop over y[a] here)
-          const float ye[4] = {y.x, y.y, y.z, y.w};
-          const int left = n_rows - 4 * q;  // 1..3
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ye[0]), ry, prow_ok ? off : kOOB, 0, 2);
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ye[1]), ry, prow_ok && left > 1 ? off + 4 : kOOB, 0, 2);
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ye[2]), ry, prow_ok && left > 2 ? off + 8 : kOOB, 0, 2);
-        }
-      }
-    }
+    const int64_t p0 = stage_of(k) * sr;
+    const float* im0 = img + (k % NBUF) * SF;
+    mix_stage<T, QPT, SAUX, COPY>(Q, im0, YT, ldy, n_rows, P, p0, xw, sr, spt, q0, g, GR, rowptr, col, val);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this stage's LDS reads are done before the next barrier
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -277,24 +297,33 @@ int dol_mix_csr_pm_f32(const float* XT, int64_t ldx, int32_t x_rows, float* YT, 
   if (n_rows == 0 || P == 0) { dol::g_err[0] = '\0'; return DOL_OK; }
   if (!XT || !YT || !rowptr || (x_rows > 0 && (!col || !val))) return fail(DOL_EINVAL, "%s: null pointer", nm);
   if (x_rows < 1) return fail(DOL_EINVAL, "%s: x_rows must be >= 1", nm);
-  if (x_rows > kStageF || n_rows > 2 * 4 * kT)
-    return fail(DOL_EINVAL, "%s: at most %d agents (x_rows %d, n_rows %d)", nm, kStageF, x_rows, n_rows);
+  if (x_rows > kMaxAgents || n_rows > kMaxAgents)
+    return fail(DOL_EINVAL, "%s: at most %d agents (x_rows %d, n_rows %d)", nm, kMaxAgents, x_rows, n_rows);
   if (ldx % 4 || ldx < (x_rows + 3) / 4 * 4 || ldy % 4 || ldy < (n_rows + 3) / 4 * 4)
     return fail(DOL_EINVAL, "%s: ldx / ldy must be multiples of 4 covering the rounded-up agent counts", nm);
   if ((reinterpret_cast<uintptr_t>(XT) | reinterpret_cast<uintptr_t>(YT)) & 15u)
     return fail(DOL_EINVAL, "%s: XT and YT must be 16-B aligned", nm);
   if (XT == YT) return fail(DOL_EINVAL, "%s: XT and YT alias (Jacobi mix needs two buffers)", nm);
   const int xw = (x_rows + 255) / 256 * 256;
-  int sr = kStageF / xw;
   const int nq = (n_rows + 3) / 4;
-  int qpt = 1, qp_log2 = 0, spt;
-  if (nq <= kT) {
+  // geometry: 1024-thread workgroups, one per CU.  Up to 4096 agents (one quad
+  // per thread): 64 KiB stages, 2 buffers; beyond (two quads per thread, a
+  // p-row up to 32 KiB): 32 KiB stages, 4 buffers.  Measured at 1024 x 2^20
+  // (one box, tools/gpu_pm_cfg.sh): 64 KiB x 2 1.511 ms, 32 KiB x 4 1.533,
+  // 48 KiB x 3 1.541; 256- / 512-thread workgroups (8 / 16 KiB stages, 2-4 per
+  // CU) 1.82 / 1.64; one stage per short-lived workgroup 4.4; a per-wave ring
+  // (no workgroup barrier, 4 KiB p-rows, 176 VGPRs) 1.64.
+  const bool big = nq > kT1 || xw > 4096;
+  const int SF = big ? 8192 : 16384, NB = big ? 4 : 2;
+  int sr = SF / xw;
+  int qp_log2 = 0, spt;
+  if (!big) {
     while ((1 << qp_log2) < nq) ++qp_log2;
-    const int gr = kT >> qp_log2;
+    const int gr = kT1 >> qp_log2;
     if (sr >= gr) sr = std::min(sr / gr * gr, 4 * gr);
     spt = (sr + gr - 1) / gr;
   } else {
-    qpt = 2;
+
     sr = 1;
     spt = 2;
   }
@@ -302,26 +331,27 @@ int dol_mix_csr_pm_f32(const float* XT, int64_t ldx, int32_t x_rows, float* YT, 
   const int64_t n_stages = (P + sr - 1) / sr;
   const int ncu = n_cus();
   if (ncu <= 0) return fail(DOL_EINVAL, "%s: no device", nm);
-  const int64_t grid = std::min<int64_t>(ncu, n_stages);
-  const int nbuf = env_int("DOL_PM_NBUF", 4) == 3 ? 3 : 4;
-  const int var = env_int("DOL_PM_VARIANT", 0);  // measurement knobs: 1 nt DMA, 2 plain stores, 3 both, 4 copy
-  auto go = [&](auto kern, int nb) {
-    const int lds = nb * kStageF * 4;
+  // measurement knobs: DOL_PM_VARIANT 1 = default-policy DMA loads, 4 = copy in
+  // this geometry (the structure's ceiling); DOL_PM_NSEG = stage-order segments
+  const int var = env_int("DOL_PM_VARIANT", 0);
+  auto go = [&](auto kern) {
+    const int lds = NB * SF * 4;
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(grid)), dim3(kT), lds, s, XT, ldx, x_rows, YT, ldy, n_rows, P,
-                       xw, sr, qp_log2, spt, n_stages, rowptr, col, val);
+    const int64_t grid = std::min<int64_t>(ncu, n_stages);
+    int nseg = env_int("DOL_PM_NSEG", 8);
+    if (nseg < 1 || grid % nseg) nseg = 1;
+    hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(grid)), dim3(kT1), lds, s, XT, ldx, x_rows, YT, ldy, n_rows, P,
+                       xw, sr, qp_log2, spt, n_stages, nseg, rowptr, col, val);
   };
-  auto pick = [&](auto qc) {
-    constexpr int Q = decltype(qc)::value;
-    if (var == 1) go(csr_pm_kernel<4, Q, 2, 2>, 4);
-    else if (var == 2) go(csr_pm_kernel<4, Q, 0, 0>, 4);
-    else if (var == 3) go(csr_pm_kernel<4, Q, 2, 0>, 4);
-    else if (var == 4) go(csr_pm_kernel<4, Q, 0, 2, true>, 4);
-    else if (nbuf == 3) go(csr_pm_kernel<3, Q>, 3);
-    else go(csr_pm_kernel<4, Q>, 4);
+  auto pick = [&](auto sfc, auto nbc, auto qc) {
+    constexpr int SFc = decltype(sfc)::value, NBc = decltype(nbc)::value, Qc = decltype(qc)::value;
+    if (var == 1) go(csr_pm_kernel<kT1, SFc, NBc, Qc, 0, 2>);
+    else if (var == 4) go(csr_pm_kernel<kT1, SFc, NBc, Qc, 2, 2, true>);
+    else go(csr_pm_kernel<kT1, SFc, NBc, Qc, 2, 2>);
   };
-  if (qpt == 1) pick(std::integral_constant<int, 1>{});
-  else pick(std::integral_constant<int, 2>{});
+  using std::integral_constant;
+  if (big) pick(integral_constant<int, 8192>{}, integral_constant<int, 4>{}, integral_constant<int, 2>{});
+  else pick(integral_constant<int, 16384>{}, integral_constant<int, 2>{}, integral_constant<int, 1>{});
   return check_launch(nm);
 }
 

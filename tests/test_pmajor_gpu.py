@@ -58,7 +58,7 @@ def test_pm_mix_matches_reference_consensus(case, gpu):
     assert bits_equal(run_pm(mix[case + "__X"], c, gpu), mix[case + "__Y"])
 
 
-@pytest.mark.parametrize("n", [5, 64, 100, 257, 1000, 1024, 1025, 2047, 4096, 5000, 8192])
+@pytest.mark.parametrize("n", [5, 64, 100, 257, 1000, 1024, 1025, 2047, 4096, 4097, 5000, 8192])
 @pytest.mark.parametrize("P", [1, 7, 300])
 def test_pm_mix_random_regular_vs_oracle(n, P, gpu):
     c = G.random_regular_csr(n, 4, seed=n + 3)
@@ -66,9 +66,11 @@ def test_pm_mix_random_regular_vs_oracle(n, P, gpu):
     assert bits_equal(run_pm(X, c, gpu, extra=4 * (n % 3)), oracle.mix_csr(X, c.rowptr, c.col, c.val))
 
 
-@pytest.mark.parametrize("nbuf", ["3", "4"])
-def test_pm_mix_ring_depths_bit_identical(nbuf, gpu, monkeypatch):
-    monkeypatch.setenv("DOL_PM_NBUF", nbuf)
+@pytest.mark.parametrize("nseg", ["1", "3", "8"])
+def test_pm_mix_stage_orders_bit_identical(nseg, gpu, monkeypatch):
+    """The stage order (DOL_PM_NSEG segments walked side by side) is a speed
+    choice only; 3 does not divide the grid and falls back to one sweep."""
+    monkeypatch.setenv("DOL_PM_NSEG", nseg)
     torch.manual_seed(2028)
     c = G.communication_csr("circle", "stochastic", 1000)[0]
     X = np.random.default_rng(1).standard_normal((1000, 2500)).astype(np.float32)

@@ -156,8 +156,9 @@ def pm_round(N, P, topo, reps, dev, X, Y):
     else:
         c = G.random_regular_csr(N, int(topo[2:]), seed=2028)
     ld = (N + 3) // 4 * 4
+    yoff = int(os.environ.get("PM_YOFF", "0"))  # floats: YT's start relative to Y's (HBM channel placement probe)
     XT = X.view(-1)[: P * ld].view(P, ld)
-    YT = Y.view(-1)[: P * ld].view(P, ld)
+    YT = Y.view(-1)[yoff: yoff + P * ld].view(P, ld)
     rp = torch.as_tensor(c.rowptr, dtype=torch.int32, device=dev)
     col = torch.as_tensor(c.col, dtype=torch.int32, device=dev)
     val = torch.as_tensor(c.val, dtype=torch.float32, device=dev)
@@ -173,6 +174,7 @@ def pm_round(N, P, topo, reps, dev, X, Y):
     ms = s_.elapsed_time(e_) / reps
     alg = 2 * N * P * 4
     print(json.dumps({"topology": topo + "-pm", "kernel": "csr_pm (parameter-major bank)", "agents": N, "params": P,
+                      "yoff": yoff, "x_ptr_mod_2M": XT.data_ptr() % (1 << 21), "y_minus_x": YT.data_ptr() - XT.data_ptr(),
                       "nnz": int(c.nnz), "ms_per_launch": ms, "rounds_per_s": 1e3 / ms,
                       "GBps": alg / (ms / 1e3) / 1e9, "frac_of_8TBps": alg / (ms / 1e3) / 1e9 / 8000.0}), flush=True)
 
