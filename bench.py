@@ -35,6 +35,11 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
+def _log(msg: str) -> None:
+    """Progress on stderr (stdout carries only the one JSON line)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 METRIC = "consensus rounds/sec at 8192 agents x 1M params (1/8 GPU) + % of HBM peak"
 HBM_PEAK_GBPS = 8000.0  # MI355X spec (MI355X_MICROARCH.md, chip-level parameters)
 
@@ -46,8 +51,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--agents", type=int, default=8192)
     ap.add_argument("--params", type=int, default=1 << 20)
-    ap.add_argument("--cpu-agents", type=int, default=256, help="CPU baseline sample size (agents)")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-agents", type=int, nargs="+", default=[64, 256, 1024],
+                    help="CPU baseline sample sizes (agents; SURVEY 8d)")
+    ap.add_argument("--cpu-seconds", type=float, default=4.0, help="CPU seconds per sample below 512 agents")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline (profiling runs)")
     ap.add_argument("--no-copy", action="store_true", help="skip the copy-kernel calibration")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_ring_8192x1M.json"))
@@ -66,103 +72,131 @@ def ring_weights(n: int):
     return rw
 
 
-def copy_peak(device, gib: float = 8.0, reps: int = 20) -> float:
+def copy_peak(device, X=None, Y=None, P=None, gib: float = 8.0, reps: int = 20) -> dict:
+    """HBM calibration: the best of three copies on this box, each timed with
+    HIP events — a flat nontemporal copy over 2 x `gib` GiB and over 2 x 16 GiB,
+    and (given the bench's own [N, ld] buffers) a copy in the ring kernel's tile
+    kernel's own access pattern over the same rows (dol_stream_copy_rows_f32:
+    the ring kernel with the stencil replaced by the row itself).  Returns every rate
+    and the winner; `frac_of_measured_copy` divides by the winner."""
     from dolhip import ops
-    n = int(gib * (1 << 30) / 4)
-    a = torch.empty(n, dtype=torch.float32, device=device).normal_()
-    b = torch.empty_like(a)
-    for _ in range(2):
-        ops.stream_copy(a, b)
-    torch.cuda.synchronize(device)
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(reps):
-        ops.stream_copy(a, b)
-    e.record()
-    torch.cuda.synchronize(device)
-    sec = s.elapsed_time(e) / 1e3 / reps
-    del a, b
-    torch.cuda.empty_cache()
-    return 2 * n * 4 / sec / 1e9
+
+    def timed(fn, nbytes):
+        for _ in range(2):
+            fn()
+        torch.cuda.synchronize(device)
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(reps):
+            fn()
+        e.record()
+        torch.cuda.synchronize(device)
+        return nbytes / (s.elapsed_time(e) / 1e3 / reps) / 1e9
+
+    out = {}
+    if X is not None:
+        out["ring_kernel_pattern_copy"] = timed(lambda: ops.stream_copy_rows(X, Y, P=P), 2 * X.shape[0] * P * 4)
+    for g in (gib, 16.0):
+        n = int(g * (1 << 30) / 4)
+        a = torch.empty(n, dtype=torch.float32, device=device).normal_()
+        b = torch.empty_like(a)
+        out[f"flat_nt_copy_{int(g)}GiB"] = timed(lambda: ops.stream_copy(a, b), 2 * n * 4)
+        del a, b
+        torch.cuda.empty_cache()
+    best = max(out, key=out.get)
+    return {"GBps": out[best], "variant": best, "all_GBps": out}
 
 
-def cpu_baseline(n_agents: int, P: int, seconds: float, full_agents: int):
+def cpu_baseline(sizes, P: int, seconds: float, full_agents: int):
+    """The reference-structured torch-CPU round (oracle/ref_cpu.py: the O(N^2)
+    Neighbors scan + consensus + load_state_dict) at each N in `sizes` (SURVEY
+    §8d: 64, 256, 1024 agents x 2^20), and the vectorised torch-CPU ring round
+    beside it, on the threads this process may use (os.sched_getaffinity; the
+    box's CPU share).  `value` extrapolates the largest N per byte to
+    `full_agents` (optimistic for the reference: its scan grows as N^2)."""
     from oracle import ref_cpu
-    threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16)
-    torch.set_num_threads(threads)
-    torch.manual_seed(2028)
     from dolhip import graph as G
-    W = G.communication_graph("circle", "stochastic", n_agents)[0]
-    X = torch.randn(n_agents, P)
-    rounds, sec = ref_cpu.time_rounds(W, X, min_seconds=seconds)
-    rate = rounds / sec
-    # per-byte extrapolation to the metric's 8192-agent system (optimistic for
-    # the reference: its O(N^2) neighbour scan grows faster than linearly)
-    value = rate * n_agents / full_agents
-    # the stronger CPU bar, same sample, whole-matrix torch ops
-    rw = G.csr_from_dense(W).ring_weights()
-    vr, vsec = ref_cpu.time_vectorized(X, torch.from_numpy(rw[0]), torch.from_numpy(rw[1]), min_seconds=seconds / 3)
-    vrate = vr / vsec
-    vectorized = {"value": vrate * n_agents / full_agents, "unit": "rounds/s", "cores": threads, "kind": "port",
-                  "sample": (f"vectorized torch-CPU ring round (oracle/ref_cpu.py: roll + mul + add over the whole "
-                             f"[{n_agents}, {P}] matrix) : {vr} rounds in {vsec:.2f} s = {vrate:.3f} rounds/s = "
-                             f"{2 * n_agents * P * 4 * vrate / 1e9:.1f} GB/s; value per-byte extrapolated to "
-                             f"{full_agents} agents")}
+    # the box's CPU share: OMP_NUM_THREADS (16 per GPU on the pool, where
+    # os.cpu_count() and the affinity mask report the whole machine); else the
+    # affinity mask
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    threads = int(os.environ.get("OMP_NUM_THREADS") or aff)
+    torch.set_num_threads(threads)
+    per_n, vec_n = {}, {}
+    for n in sizes:
+        _log(f"cpu baseline: {n} agents x {P} on {threads} threads")
+        torch.manual_seed(2028)
+        W = G.communication_graph("circle", "stochastic", n)[0]
+        X = torch.randn(n, P)
+        # one warm-up round below 512 agents; the big sample times exactly one round
+        rounds, sec = ref_cpu.time_rounds(W, X, min_seconds=seconds if n < 512 else 0.0,
+                                          max_rounds=50 if n < 512 else 1, warmup=n < 512)
+        per_n[n] = {"rounds": rounds, "seconds": sec, "rounds_per_s": rounds / sec,
+                    "GBps": 2 * n * P * 4 * rounds / sec / 1e9}
+        rw = G.csr_from_dense(W).ring_weights()
+        vr, vsec = ref_cpu.time_vectorized(X, torch.from_numpy(rw[0]), torch.from_numpy(rw[1]),
+                                           min_seconds=seconds / 3)
+        vec_n[n] = {"rounds": vr, "seconds": vsec, "rounds_per_s": vr / vsec, "GBps": 2 * n * P * 4 * vr / vsec / 1e9}
+        del W, X
+    big = max(sizes)
+    value = per_n[big]["rounds_per_s"] * big / full_agents
     return {
         "value": value,
         "unit": "rounds/s",
         "cores": threads,
+        "os_cpu_count": os.cpu_count(),
+        "affinity_cpus": aff,
         "kind": "port",
-        "vectorized": vectorized,
+        "per_agents": per_n,
+        "vectorized": {"value": vec_n[big]["rounds_per_s"] * big / full_agents, "unit": "rounds/s", "cores": threads,
+                       "kind": "port", "per_agents": vec_n,
+                       "sample": "vectorized torch-CPU ring round (oracle/ref_cpu.py: roll + mul + add over the whole "
+                                 "matrix); value per-byte extrapolated from the largest N"},
         "sample": (f"reference-structured torch-CPU round (Neighbors scan + consensus + load_state_dict, "
-                   f"oracle/ref_cpu.py) on {n_agents} agents x {P} params, circle/stochastic: {rounds} rounds "
-                   f"in {sec:.2f} s = {rate:.3f} rounds/s; value = that x {n_agents}/{full_agents} "
-                   f"(per-byte extrapolation to {full_agents} agents)"),
+                   f"oracle/ref_cpu.py), circle/stochastic, N in {list(sizes)} x {P} params on {threads} threads; "
+                   f"value = the N={big} rate x {big}/{full_agents} (per-byte extrapolation to {full_agents} agents)"),
     }
 
 
-def primal_dual_round(N: int, P: int, world: int, rank: int, device, steps: int):
-    """Secondary measurement (BASELINE config 4, ADMM side): one FedADMM round
-    over ALL agents = the local step (ADMM gradient term + momentum SGD,
-    DEC/clients.py:125-139 + SGD.step) fused with the dual ascent that follows
-    it (:141-144) in dol_admm_step_dual_f32, then the global mean of the new weights
-    (ordered sum of the local rows + all_reduce across ranks + /N,
-    DEC/servers.py:42-48).  Timed like the headline (barrier, max over
+def primal_dual_round(N: int, P: int, world: int, rank: int, device, steps: int, local_steps: int = 10):
+    """Secondary measurement (BASELINE config 4, primal/dual side): one FedADMM
+    round of dolhip.synthetic.SeparableADMM on least squares over ALL N agents
+    (frac = 1), `local_steps` local momentum-SGD steps per client in registers:
+    the fused client round (dol_admm_ls_round_f32: w = theta, ADMM gradient +
+    SGD steps, dual ascent, ||w - theta||^2 / ||alpha||^2 partials) over the
+    local agent block, then the server mean — local ordered sum + all_reduce
+    (RCCL) + / N ("fast"; DEC/servers.py:42-48's order is the "exact" mode).
+    Bit-exact against the reference's own FedAdmm_Server on a least-squares
+    model (tests/test_admm_gpu.py).  Timed like the headline (barrier, max over
     ranks); each kernel's share from HIP events."""
-    from dolhip import bank as B, ops, parallel
-    lo, hi = parallel.shard_bounds(N, world, rank)
-    n = hi - lo
-    ld = B.row_stride(P)
-    g = torch.Generator(device=device).manual_seed(7 + rank)
-    bufs = {k: torch.empty(n, ld, dtype=torch.float32, device=device) for k in ("w", "g", "mom", "alpha")}
-    for t in bufs.values():
-        t.normal_(generator=g)
-    theta = torch.empty(ld, dtype=torch.float32, device=device).normal_(generator=g)
-    order = torch.arange(n, dtype=torch.int32, device=device)
-    names = ("step_dual", "mean")
+    from dolhip import ops
+    from dolhip.synthetic import SeparableADMM
+    prob = SeparableADMM(N, P, rho=0.1, lr=0.1, momentum=0.5, local_steps=local_steps, frac=1.0, seed=2028,
+                         device=device, mean="fast")
     ev = {k: [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
-          for k in names}
+          for k in ("client_round", "mean")}
+    rnd, osum = ops.admm_ls_round, ops.ordered_sum
+    state = {"k": None}
 
-    def one(k=None):
-        e = (lambda nm: ev[nm][k]) if k is not None else (lambda nm: None)
-        def rec(nm, i):
-            if e(nm):
-                e(nm)[i].record()
-        rec("step_dual", 0)
-        ops.admm_step_dual(bufs["w"], bufs["g"], theta, bufs["alpha"], buf=bufs["mom"], rho=0.1, lr=0.1,
-                           momentum=0.5, first_step=False, write_grad=False, P=P)
-        rec("step_dual", 1)
-        rec("mean", 0)
-        parallel.global_mean(bufs["w"], order, N, P, out=theta)
-        rec("mean", 1)
+    def timed_round(*a, **kw):
+        k = state["k"]
+        if k is not None:
+            ev["client_round"][k][0].record()
+        rnd(*a, **kw)
+        if k is not None:
+            ev["client_round"][k][1].record()
+            ev["mean"][k][0].record()
 
-    one()
+    prob._round = timed_round
+    prob.round()  # warm-up (first momentum step)
     torch.cuda.synchronize(device)
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
     for k in range(steps):
-        one(k)
+        state["k"] = k
+        prob.round()
+        ev["mean"][k][1].record()
     torch.cuda.synchronize(device)
     if world > 1:
         dist.barrier()
@@ -170,21 +204,51 @@ def primal_dual_round(N: int, P: int, world: int, rank: int, device, steps: int)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     el = float(el.item())
+    n = prob.n
     row_bytes = n * P * 4
-    # compulsory bytes per launch: step+dual reads w, g, buf, alpha and writes w, buf, alpha
-    alg = {"step_dual": 7 * row_bytes, "mean": row_bytes + P * 4}
+    # compulsory bytes: client round reads t, alpha, buf and writes w, alpha, buf; the mean reads w, writes theta
+    alg = {"client_round": 6 * row_bytes, "mean": row_bytes + P * 4}
     kern = {}
-    for nm in names:
+    for nm in alg:
         ms = float(np.mean([a.elapsed_time(b) for a, b in ev[nm]]))
         kern[nm] = {"ms": ms, "GBps": alg[nm] / (ms / 1e3) / 1e9, "frac": alg[nm] / (ms / 1e3) / 1e9 / HBM_PEAK_GBPS,
                     "algorithmic_bytes": alg[nm]}
-    for t in bufs.values():
-        del t
-    bufs.clear()
+    hist = prob.history
+    out = {"rounds_per_s": steps / el, "ms_per_round": el / steps * 1e3, "agents": N, "params": P,
+           "local_steps": local_steps, "kernels": kern,
+           "primal_resid_sq_last": hist[-1]["primal_resid_sq"], "dual_sq_last": hist[-1]["dual_sq"],
+           "what": "FedADMM least-squares round over all agents: fused client round (w = theta, %d momentum-SGD "
+                   "steps with the ADMM term, dual ascent) + all_reduce mean" % local_steps}
+    del prob
     torch.cuda.empty_cache()
-    return {"rounds_per_s": steps / el, "ms_per_round": el / steps * 1e3, "agents": N, "params": P,
-            "what": "ADMM-grad + momentum-SGD step fused with the dual ascent, then global mean (all agents)",
-            "kernels": kern}
+    return out
+
+
+def random_regular_pm_round(device, X, Y, N: int, P: int, reps: int = 10):
+    """Secondary (BASELINE config 3's random-regular mix at the headline size):
+    X <- W X for a random 4-regular W on the parameter-major bank
+    (dol_mix_csr_pm_f32), reusing the headline's buffers as XT [P, N] / YT."""
+    from dolhip import graph as G, ops
+    c = G.random_regular_csr(N, 4, seed=2028)
+    XT = X.view(-1)[: P * N].view(P, N)
+    YT = Y.view(-1)[: P * N].view(P, N)
+    rp = torch.as_tensor(c.rowptr, device=device)
+    col = torch.as_tensor(c.col, device=device)
+    val = torch.as_tensor(c.val, device=device)
+    for _ in range(2):
+        ops.mix_csr_pm(XT, YT, rp, col, val)
+    torch.cuda.synchronize(device)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        ops.mix_csr_pm(XT, YT, rp, col, val)
+    e.record()
+    torch.cuda.synchronize(device)
+    ms = s.elapsed_time(e) / reps
+    gbps = 2 * N * P * 4 / (ms / 1e3) / 1e9
+    return {"agents": N, "params": P, "degree": 4, "ms_per_round": ms, "rounds_per_s": 1e3 / ms, "GBps": gbps,
+            "frac": gbps / HBM_PEAK_GBPS, "kernel": "csr_pm_kernel (parameter-major bank)",
+            "what": "random 4-regular W mix on the parameter-major bank, bit-identical to the reference consensus"}
 
 
 def dense_mix_round(device, N: int = 1024, P: int = 101770, reps: int = 10):
@@ -247,6 +311,7 @@ def main():
     ring.x.normal_(generator=g)
     ring.y.zero_()
 
+    _log(f"ring {N} x {P}: warm-up")
     for _ in range(args.warmup):
         ring.step()
     torch.cuda.synchronize(device)
@@ -302,17 +367,27 @@ def main():
                    "GBps_per_pass": 2 * N * P * 4 / (ms_pass / 1e3) / 1e9,
                    "what": "FedLCon eps=5 consensus rounds fused into one HBM pass (ring_steps_kernel), bit-identical"}
 
-    copy_gbps = None
+    # secondary (N = 1): config 3's random 4-regular mix at the headline size on
+    # the parameter-major bank, in the headline's buffers
+    _log("headline done")
+    rr_pm = None
+    if world == 1 and not args.no_primal_dual and N <= 8192:
+        rr_pm = random_regular_pm_round(device, ring.x, ring.y, N, P)
+    _log("random-regular pm done")
+    calib = None
+    if not args.no_copy:
+        calib = copy_peak(device, ring.x, ring.y, P)
     del ring.x, ring.y
     torch.cuda.empty_cache()
-    if not args.no_copy:
-        copy_gbps = copy_peak(device)
+    _log("calibration done")
     pd_round = None
     if not args.no_primal_dual:
         pd_round = primal_dual_round(N, P, world, rank, device, args.pd_steps)
+    _log("primal/dual round done")
     dense = None
     if world == 1 and not args.no_primal_dual:
         dense = dense_mix_round(device)
+    _log("dense ER done")
 
     traffic = None
     traffic_src = None
@@ -367,12 +442,14 @@ def main():
                 "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": alg_bytes,
                 "kernel_ms": kern_ms,
-                "copy_kernel_GBps": copy_gbps,
-                "frac_of_measured_copy": (achieved / copy_gbps) if copy_gbps else None,
+                "copy_kernel_GBps": calib["GBps"] if calib else None,
+                "copy_calibration": calib,
+                "frac_of_measured_copy": (achieved / calib["GBps"]) if calib else None,
             },
             "cpu_baseline": cpu,
             "primal_dual_round": pd_round,
             "fedlcon_eps5": fedlcon,
+            "random_regular_pm": rr_pm,
             "dense_er_mix": dense,
         }
         print(json.dumps(out), flush=True)

@@ -259,7 +259,10 @@ __global__ __launch_bounds__(kThreads) void ring_mix_kernel(
 #define DOL_GPTR(p) ((const __attribute__((address_space(1))) void*)(p))
 #define DOL_LPTR(p) ((__attribute__((address_space(3))) void*)(p))
 
-template <int R, class Epi = NoEpi, bool NTI = false>
+// COPY (roofline calibration only): the same loads, cache policies and stores,
+// with the stencil replaced by the tile's own row (Y = X): the memory-system
+// ceiling of exactly this kernel's access pattern.
+template <int R, class Epi = NoEpi, bool NTI = false, bool COPY = false>
 __global__ __launch_bounds__(kThreads) void ring_mix_dma_kernel(
     const float* __restrict__ X, int64_t ldx, float* __restrict__ Y, int64_t ldy, int n_rows,
     int64_t ncols_v, int64_t n_col_tiles, const float* __restrict__ halo_prev,
@@ -296,7 +299,7 @@ __global__ __launch_bounds__(kThreads) void ring_mix_dma_kernel(
   for (int k = 0; k < R; ++k) {
     const int r = r0 + k;
     if (r < r1)
-      __builtin_nontemporal_store(epi.apply(axpy0(wprev[r], v[k], wnext[r], v[k + 2]), es[k], r, 4 * c),
+      __builtin_nontemporal_store(COPY ? v[k + 1] : epi.apply(axpy0(wprev[r], v[k], wnext[r], v[k + 2]), es[k], r, 4 * c),
                                   reinterpret_cast<f4*>(Y + int64_t(r) * ldy) + c);
   }
 }
@@ -487,384 +490,6 @@ __global__ __launch_bounds__(kThreads) void csr_xcd_kernel(
       acc = epi.apply(acc, es, r, 4 * c);
       __builtin_nontemporal_store(acc, reinterpret_cast<f4*>(Y + int64_t(r) * ldy) + c);
     }
-  }
-}
-
-// ----------------------------------------------------------------------------
-// LDS-slab CSR mix (graphs of up to 4096 agents, any W): the column slab
-// X[0..x_rows)[16L bytes] of every agent is staged in the CU's LDS, so each X
-// byte is read from memory ONCE per round however many rows gather it, and
-// the deg gathers per output row are LDS reads.  One persistent 1024-thread
-// workgroup per CU walks slabs with two 64 KiB images: the LDS-DMA
-// (global_load_lds_dwordx4, no registers) of slab t+1 flies while slab t is
-// summed.  Each thread owns PER = 4 lane-rows (row = k * 1024/L + tid / L,
-// 16-B piece tid % L) for the fill AND the output, and keeps those rows'
-// first four neighbour indices / weights in registers for the whole kernel
-// (the index chain is paid once, not per tile).  Slab order is XCD-aware: at
-// step t workgroup w of XCD x (= blockIdx % 8, a speed assumption only) takes
-// slab (t*8 + x)*nw + w, so one XCD's workgroups read adjacent pieces of the
-// same rows together.  Sums: +0 start, ascending CSR order, no FMA — the
-// arithmetic of csr_mix_kernel (bit-identical).  Rows with more than four
-// neighbours read the rest of their (col, val) list from memory.
-// ----------------------------------------------------------------------------
-constexpr int kLdsImgBytes = 64 * 1024;  // one image; two are double-buffered
-constexpr int kLdsT = 1024;              // threads per LDS-slab workgroup
-
-template <int L, bool NT_STORE, class Epi = NoEpi>
-__global__ __launch_bounds__(kLdsT) void csr_lds_kernel(
-    const float* __restrict__ X, int64_t ldx, int x_rows, float* __restrict__ Y, int64_t ldy, int n_rows,
-    int64_t n_slabs, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
-    const float* __restrict__ val, Epi epi) {
-  constexpr int ROWS = kLdsImgBytes / (16 * L);  // rows an image holds (4096 / L)
-  constexpr int RSTEP = kLdsT / L;               // rows per lane-row step
-  constexpr int PER = ROWS / RSTEP;              // lane-rows per thread (4)
-  constexpr int DMAX = 4;                        // neighbours held in registers per row
-  constexpr int IMG = (ROWS + 1) * L;            // f4 per image incl. its zero row
-  // two images, each followed by a zero row: register slots past a row's
-  // degree point at column ROWS (the zero row) with weight +0, and
-  // acc + (+0 * +0) == acc for every acc this sum can hold (it starts at +0,
-  // so it is never -0): short rows need no per-entry branch
-  extern __shared__ __attribute__((aligned(16))) f4 img[];
-  const int tid = threadIdx.x;
-  const int piece = tid % L, rsub = tid / L;
-  if (tid < 2 * L) img[(tid / L) * IMG + ROWS * L + tid % L] = f4{0.f, 0.f, 0.f, 0.f};
-
-  uint32_t cc[PER][DMAX / 2];  // columns, two 16-bit indices per register
-  float ww[PER][DMAX];
-  uint32_t longm = 0;          // bit k: lane-row k has more than DMAX neighbours
-#pragma unroll
-  for (int k = 0; k < PER; ++k) {
-    const int r = k * RSTEP + rsub;
-    const int rc = r < n_rows ? r : 0;
-    const int e0 = rowptr[rc];
-    const int dg = r < n_rows ? rowptr[rc + 1] - e0 : 0;
-    longm |= uint32_t(dg > DMAX) << k;
-#pragma unroll
-    for (int q = 0; q < DMAX; ++q) {
-      const bool in = q < dg;
-      const int e = in ? e0 + q : 0;
-      const uint32_t cq = in ? static_cast<uint32_t>(col[e]) : uint32_t(ROWS);
-      if (q % 2 == 0) cc[k][q / 2] = cq;
-      else cc[k][q / 2] |= cq << 16;
-      ww[k][q] = in ? val[e] : 0.0f;
-    }
-  }
-
-  const uint32_t xcd = blockIdx.x & 7u, wl = blockIdx.x >> 3, nw = gridDim.x >> 3;
-  auto slab = [&](int64_t t) -> int64_t { return (t * 8 + xcd) * nw + wl; };
-  // DMA sources = wave-uniform 64-bit row base + 32-bit lane offset (the host
-  // checks 64 * ld * 4 < 2^32).  Every lane loads, without a branch: a wave
-  // whose rows start past x_rows re-reads row x_rows - 1, a lane past x_rows
-  // its wave's first row, into image slots no column refers to.
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int lane = tid & 63;
-  const int wrow = wave * (64 / L);  // the wave's first row within a step
-  const uint32_t xoff = static_cast<uint32_t>(((lane / L) * ldx + piece * 4) * 4);
-  const uint32_t yoff = static_cast<uint32_t>(((lane / L) * ldy + piece * 4) * 4);
-  auto fill = [&](int64_t s, int b) {
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const int wr = min(k * RSTEP + wrow, x_rows - 1);
-      const uint32_t lo = k * RSTEP + rsub < x_rows ? xoff : static_cast<uint32_t>(piece * 16);
-      const char* src = reinterpret_cast<const char*>(X + (int64_t(wr) * ldx + s * L * 4)) + lo;
-      __builtin_amdgcn_global_load_lds(DOL_GPTR(src), DOL_LPTR(&img[b * IMG + (k * RSTEP + wrow) * L]), 16, 0, 0);
-    }
-  };
-  if (slab(0) < n_slabs) fill(slab(0), 0);
-  for (int64_t t = 0;; ++t) {
-    const int64_t s = slab(t);
-    if (s >= n_slabs) break;
-    const int b = static_cast<int>(t & 1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this slab's DMA (and the last slab's stores)
-    __syncthreads();
-    if (slab(t + 1) < n_slabs) fill(slab(t + 1), b ^ 1);  // the image read two slabs ago
-    const f4* im = img + b * IMG;
-    const int64_t cf = (s * L + piece) * 4;  // absolute float column of this lane's piece
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const int r = k * RSTEP + rsub;
-      if (r < n_rows) {
-        const auto es = epi.template load<f4>(r, cf);
-        f4 acc = f4{0.f, 0.f, 0.f, 0.f};
-        acc = fmac(acc, ww[k][0], im[(cc[k][0] & 0xffffu) * L + piece]);
-        acc = fmac(acc, ww[k][1], im[(cc[k][0] >> 16) * L + piece]);
-        acc = fmac(acc, ww[k][2], im[(cc[k][1] & 0xffffu) * L + piece]);
-        acc = fmac(acc, ww[k][3], im[(cc[k][1] >> 16) * L + piece]);
-        if (longm & (1u << k)) {  // long rows: the rest of the list from memory
-          const int e1 = rowptr[r + 1];
-          for (int e = rowptr[r] + DMAX; e < e1; ++e) acc = fmac(acc, val[e], im[col[e] * L + piece]);
-        }
-        acc = epi.apply(acc, es, r, cf);
-        char* yb = reinterpret_cast<char*>(Y + (int64_t(k * RSTEP + wrow) * ldy + s * L * 4));
-        stv<f4, NT_STORE>(reinterpret_cast<f4*>(yb + yoff), acc);
-      }
-    }
-  }
-}
-
-// ----------------------------------------------------------------------------
-// LDS-slab CSR mix, register-staged, for graphs of up to 1024 agents: one
-// 128-B column slab of every agent (128 KiB) plus the whole graph's index
-// (first four columns as u16, weights as fp32: 24 KiB) live in LDS.  One
-// persistent 1024-thread workgroup per CU; each thread owns 8 lane-rows
-// (row = k * 128 + tid / 8, 16-B piece tid % 8) for the fill and the output.
-// The next slab is loaded into registers while the current one is summed.
-// Column 1024 is an all-zero row that pads short rows (see csr_lds_kernel);
-// bit 15 of a row's first column marks a row with more than four neighbours,
-// whose remaining entries come from memory.  Sums as csr_mix_kernel.
-// ----------------------------------------------------------------------------
-constexpr int kLds8Rows = 1024;
-constexpr int kLds8Bytes = (kLds8Rows + 1) * 128 + kLds8Rows * (16 + 8);
-
-template <bool NT_STORE, class Epi = NoEpi>
-__global__ __launch_bounds__(1024) void csr_lds8_kernel(
-    const float* __restrict__ X, int64_t ldx, int x_rows, float* __restrict__ Y, int64_t ldy, int n_rows,
-    int64_t n_slabs, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
-    const float* __restrict__ val, Epi epi) {
-  constexpr int L = 8, RSTEP = 128, PER = 8, ZROW = kLds8Rows;
-  extern __shared__ __attribute__((aligned(16))) f4 img[];  // [(1024 + 1) * 8]
-  f4* wts = img + (kLds8Rows + 1) * L;                        // [1024] x 4 weights
-  uint2* cols = reinterpret_cast<uint2*>(wts + kLds8Rows);    // [1024] x 4 u16 columns
-  const int tid = threadIdx.x;
-  const int piece = tid % L, rsub = tid / L;
-  if (tid < L) img[ZROW * L + tid] = f4{0.f, 0.f, 0.f, 0.f};
-  {  // the graph's index: thread tid stages row tid
-    const int r = tid;
-    const int e0 = r < n_rows ? rowptr[r] : 0;
-    const int dg = r < n_rows ? rowptr[r + 1] - e0 : 0;
-    uint32_t c[4];
-    float w[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const bool in = q < dg;
-      c[q] = in ? static_cast<uint32_t>(col[e0 + q]) : uint32_t(ZROW);
-      w[q] = in ? val[e0 + q] : 0.0f;
-    }
-    if (dg > 4) c[0] |= 0x8000u;
-    wts[r] = f4{w[0], w[1], w[2], w[3]};
-    cols[r] = uint2{c[0] | (c[1] << 16), c[2] | (c[3] << 16)};
-  }
-  const uint32_t xcd = blockIdx.x & 7u, wl = blockIdx.x >> 3, nw = gridDim.x >> 3;
-  auto slab = [&](int64_t t) -> int64_t { return (t * 8 + xcd) * nw + wl; };
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int lane = tid & 63;
-  const int wrow = wave * (64 / L);
-  const uint32_t xoff = static_cast<uint32_t>(((lane / L) * ldx + piece * 4) * 4);
-  const uint32_t yoff = static_cast<uint32_t>(((lane / L) * ldy + piece * 4) * 4);
-  f4 pf[PER];
-  // every lane loads, without a branch (rows past x_rows: see csr_lds_kernel)
-  auto fetch = [&](int64_t s) {
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const int wr = min(k * RSTEP + wrow, x_rows - 1);
-      const uint32_t lo = k * RSTEP + rsub < x_rows ? xoff : static_cast<uint32_t>(piece * 16);
-      pf[k] = *reinterpret_cast<const f4*>(reinterpret_cast<const char*>(X + (int64_t(wr) * ldx + s * L * 4)) + lo);
-    }
-  };
-  if (slab(0) < n_slabs) fetch(slab(0));
-  for (int64_t t = 0;; ++t) {
-    const int64_t s = slab(t);
-    if (s >= n_slabs) break;
-#pragma unroll
-    for (int k = 0; k < PER; ++k) img[(k * RSTEP + rsub) * L + piece] = pf[k];
-    if (slab(t + 1) < n_slabs) fetch(slab(t + 1));
-    __syncthreads();
-    const int64_t cf = (s * L + piece) * 4;
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const int r = k * RSTEP + rsub;
-      if (r < n_rows) {
-        const uint2 c = cols[r];
-        const f4 w = wts[r];
-        const auto es = epi.template load<f4>(r, cf);
-        f4 acc = f4{0.f, 0.f, 0.f, 0.f};
-        acc = fmac(acc, w.x, img[(c.x & 0x7fffu) * L + piece]);
-        acc = fmac(acc, w.y, img[(c.x >> 16) * L + piece]);
-        acc = fmac(acc, w.z, img[(c.y & 0xffffu) * L + piece]);
-        acc = fmac(acc, w.w, img[(c.y >> 16) * L + piece]);
-        if (c.x & 0x8000u) {  // long rows: the rest of the list from memory
-          const int e1 = rowptr[r + 1];
-          for (int e = rowptr[r] + 4; e < e1; ++e) acc = fmac(acc, val[e], img[col[e] * L + piece]);
-        }
-        acc = epi.apply(acc, es, r, cf);
-        char* yb = reinterpret_cast<char*>(Y + (int64_t(k * RSTEP + wrow) * ldy + s * L * 4));
-        stv<f4, NT_STORE>(reinterpret_cast<f4*>(yb + yoff), acc);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    __syncthreads();
-  }
-}
-
-// ----------------------------------------------------------------------------
-// Two-workgroups-per-CU form of csr_lds8_kernel for graphs of up to 1024
-// agents: 64-B slabs (a 64 KiB image per workgroup), the rows' first four
-// neighbours in registers, 512 threads x 8 lane-rows; while one workgroup
-// waits at its barrier the other streams.  Same arithmetic (bit-identical).
-// ----------------------------------------------------------------------------
-template <bool NT_STORE, class Epi = NoEpi>
-__global__ __launch_bounds__(512, 2) void csr_lds2w_kernel(
-    const float* __restrict__ X, int64_t ldx, int x_rows, float* __restrict__ Y, int64_t ldy, int n_rows,
-    int64_t n_slabs, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
-    const float* __restrict__ val, Epi epi) {
-  constexpr int L = 4, T = 512, ROWS = 1024, RSTEP = T / L, PER = ROWS / RSTEP, ZROW = ROWS;
-  extern __shared__ __attribute__((aligned(16))) f4 img[];  // [(1024 + 1) * 4]
-  const int tid = threadIdx.x;
-  const int piece = tid % L, rsub = tid / L;
-  if (tid < L) img[ZROW * L + tid] = f4{0.f, 0.f, 0.f, 0.f};
-  uint32_t cc[PER][2];
-  float ww[PER][4];
-  uint32_t longm = 0;
-#pragma unroll
-  for (int k = 0; k < PER; ++k) {
-    const int r = k * RSTEP + rsub;
-    const int e0 = r < n_rows ? rowptr[r] : 0;
-    const int dg = r < n_rows ? rowptr[r + 1] - e0 : 0;
-    longm |= uint32_t(dg > 4) << k;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const bool in = q < dg;
-      const uint32_t cq = in ? static_cast<uint32_t>(col[e0 + q]) : uint32_t(ZROW);
-      if (q % 2 == 0) cc[k][q / 2] = cq;
-      else cc[k][q / 2] |= cq << 16;
-      ww[k][q] = in ? val[e0 + q] : 0.0f;
-    }
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  const uint32_t xcd = blockIdx.x & 7u, wl = blockIdx.x >> 3, nw = gridDim.x >> 3;
-  auto slab = [&](int64_t t) -> int64_t { return (t * 8 + xcd) * nw + wl; };
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int lane = tid & 63;
-  const int wrow = wave * (64 / L);
-  const uint32_t xoff = static_cast<uint32_t>(((lane / L) * ldx + piece * 4) * 4);
-  const uint32_t yoff = static_cast<uint32_t>(((lane / L) * ldy + piece * 4) * 4);
-  f4 pf[PER];
-  auto fetch = [&](int64_t s) {
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const int wr = min(k * RSTEP + wrow, x_rows - 1);
-      uint32_t lo = k * RSTEP + rsub < x_rows ? xoff : static_cast<uint32_t>(piece * 16);
-      asm volatile("" : "+v"(lo));
-      pf[k] = *reinterpret_cast<const f4*>(reinterpret_cast<const char*>(X + (int64_t(wr) * ldx + s * L * 4)) + lo);
-    }
-  };
-  if (slab(0) < n_slabs) fetch(slab(0));
-  for (int64_t t = 0;; ++t) {
-    const int64_t s = slab(t);
-    if (s >= n_slabs) break;
-#pragma unroll
-    for (int k = 0; k < PER; ++k) img[(k * RSTEP + rsub) * L + piece] = pf[k];
-    if (slab(t + 1) < n_slabs) fetch(slab(t + 1));
-    __syncthreads();
-    const int64_t cf = (s * L + piece) * 4;
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const int r = k * RSTEP + rsub;
-      if (r < n_rows) {
-        uint32_t c01 = cc[k][0], c23 = cc[k][1];
-        float w0 = ww[k][0], w1 = ww[k][1], w2 = ww[k][2], w3 = ww[k][3];
-        asm volatile("" : "+v"(c01), "+v"(c23), "+v"(w0), "+v"(w1), "+v"(w2), "+v"(w3));
-        const auto es = epi.template load<f4>(r, cf);
-        f4 acc = f4{0.f, 0.f, 0.f, 0.f};
-        acc = fmac(acc, w0, img[(c01 & 0xffffu) * L + piece]);
-        acc = fmac(acc, w1, img[(c01 >> 16) * L + piece]);
-        acc = fmac(acc, w2, img[(c23 & 0xffffu) * L + piece]);
-        acc = fmac(acc, w3, img[(c23 >> 16) * L + piece]);
-        if (longm & (1u << k)) {
-          const int e1 = rowptr[r + 1];
-          for (int e = rowptr[r] + 4; e < e1; ++e) acc = fmac(acc, val[e], img[col[e] * L + piece]);
-        }
-        acc = epi.apply(acc, es, r, cf);
-        char* yb = reinterpret_cast<char*>(Y + (int64_t(k * RSTEP + wrow) * ldy + s * L * 4));
-        stv<f4, NT_STORE>(reinterpret_cast<f4*>(yb + yoff), acc);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    __syncthreads();
-  }
-}
-
-// ----------------------------------------------------------------------------
-// Persistent L2-gather CSR mix (large graphs, any W): one 1024-thread
-// workgroup per CU owns a fixed block of output rows and keeps their first
-// four neighbours' row offsets / weights in registers for the whole kernel;
-// the workgroups of XCD x walk column tiles x, x+8, x+16, ... (TW f4 = 16*TW
-// bytes of every row) in the same order, so one tile's slab (n x 16*TW B,
-// 1 MiB at 8192 agents and 128-B tiles) is fetched from HBM into that XCD's
-// L2 once and its deg re-reads hit there.  The next tile's gathers are issued
-// before the current tile's sums (register double buffer).  No index chain
-// per tile; the slab working set is two tiles.  Sums as csr_mix_kernel.
-// ----------------------------------------------------------------------------
-template <int TW, int RPT, class Epi = NoEpi>
-__global__ __launch_bounds__(1024) void csr_xcdp_kernel(
-    const float* __restrict__ X, int64_t ldx, float* __restrict__ Y, int64_t ldy, int n_rows, int rows_per_wg,
-    int64_t n_tiles, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
-    const float* __restrict__ val, Epi epi) {
-  constexpr int RSTEP = 1024 / TW;
-  constexpr int DMAX = 4;
-  const int tid = threadIdx.x;
-  const int piece = tid % TW, rsub = tid / TW;
-  const uint32_t xcd = blockIdx.x & 7u, wl = blockIdx.x >> 3;
-  const int row0 = static_cast<int>(wl) * rows_per_wg;
-  uint32_t off[RPT][DMAX];  // each neighbour row's offset (+ this lane's piece) in 16-B units
-  float ww[RPT][DMAX];
-  uint32_t dgm = 0;        // 4 bits per lane-row: min(degree, 15)
-#pragma unroll
-  for (int k = 0; k < RPT; ++k) {
-    const int r = row0 + k * RSTEP + rsub;
-    const bool live = r < n_rows && k * RSTEP + rsub < rows_per_wg;
-    const int rc = live ? r : 0;
-    const int e0 = rowptr[rc];
-    const int dg = live ? rowptr[rc + 1] - e0 : 0;
-    dgm |= uint32_t(dg < 15 ? dg : 15) << (4 * k);
-#pragma unroll
-    for (int q = 0; q < DMAX; ++q) {
-      const bool in = q < dg;
-      const int e = in ? e0 + q : 0;
-      off[k][q] = static_cast<uint32_t>((int64_t(in ? col[e] : 0) * ldx + piece * 4) / 4);
-      ww[k][q] = in ? val[e] : 0.0f;
-    }
-  }
-  f4 g[2][RPT][DMAX];
-  auto gather = [&](int64_t tile, f4 (&dst)[RPT][DMAX]) {
-    const char* base = reinterpret_cast<const char*>(X + tile * TW * 4);
-#pragma unroll
-    for (int k = 0; k < RPT; ++k)
-#pragma unroll
-      for (int q = 0; q < DMAX; ++q) dst[k][q] = *reinterpret_cast<const f4*>(base + uint64_t(off[k][q]) * 16);
-  };
-  auto finish = [&](int64_t tile, f4 (&src)[RPT][DMAX]) {
-    const int64_t cf = (tile * TW + piece) * 4;
-#pragma unroll
-    for (int k = 0; k < RPT; ++k) {
-      const int r = row0 + k * RSTEP + rsub;
-      if (r < n_rows && k * RSTEP + rsub < rows_per_wg) {
-        const int dg = static_cast<int>((dgm >> (4 * k)) & 15u);
-        const auto es = epi.template load<f4>(r, cf);
-        f4 acc = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int q = 0; q < DMAX; ++q) {
-          const f4 x = q < dg ? src[k][q] : f4{0.f, 0.f, 0.f, 0.f};  // +0 * +0: a no-op term
-          acc = fmac(acc, ww[k][q], x);
-        }
-        if (dg > DMAX) {
-          const int e1 = rowptr[r + 1];
-          for (int e = rowptr[r] + DMAX; e < e1; ++e)
-            acc = fmac(acc, val[e], *reinterpret_cast<const f4*>(X + int64_t(col[e]) * ldx + cf));
-        }
-        acc = epi.apply(acc, es, r, cf);
-        __builtin_nontemporal_store(acc, reinterpret_cast<f4*>(Y + int64_t(r) * ldy + cf));
-      }
-    }
-  };
-  int64_t t = xcd;
-  if (t < n_tiles) gather(t, g[0]);
-  for (; t < n_tiles; t += 16) {
-    if (t + 8 < n_tiles) gather(t + 8, g[1]);
-    finish(t, g[0]);
-    if (t + 8 >= n_tiles) break;
-    if (t + 16 < n_tiles) gather(t + 16, g[0]);
-    finish(t + 8, g[1]);
   }
 }
 
@@ -1419,103 +1044,12 @@ int mix_csr_impl(const char* nm, const float* X, int64_t ldx, int32_t x_rows, fl
   const ColSplit cs = split_cols(P, vec_ok);
   constexpr int RPB = 16;
   constexpr int XW = 32, XPASSES = 2;  // XCD-pinned tiles: 512 B of a row, 16 rows per block
-  // 0 = 4 KiB tiles, 1 = XCD-pinned, 3 = LDS slab
+  // 0 = 4 KiB tiles, 1 = XCD-pinned (DOL_CSR_MODE; default: XCD-pinned from 512 rows)
   const int mode = env_int("DOL_CSR_MODE", -1);
   if (cdiv(cs.n4, kThreads) * cdiv(n_rows, RPB) > kMaxBlocks)
     return fail(DOL_EINVAL, "%s: problem too large for one launch", nm);
   int64_t done4 = 0;
-  // LDS slab: the widest 16L-byte slab whose x_rows-row image fits 64 KiB
-  const int rows_max = std::max(n_rows, x_rows);
-  const int lds_l = rows_max <= 512 ? 8 : rows_max <= 1024 ? 4 : rows_max <= 2048 ? 2 : rows_max <= 4096 ? 1 : 0;
-  static const int n_cu = [] {
-    int dev = 0, cu = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      cu = 0;
-    return cu;
-  }();
-  // one workgroup per CU; DOL_CSR_LDS_GRID (a multiple of 8) overrides it so
-  // small test shapes exercise the kernel too
-  const int grid_env = env_int("DOL_CSR_LDS_GRID", 0);
-  const int lds_grid = grid_env >= 8 ? grid_env / 8 * 8 : (n_cu >= 8 ? n_cu / 8 * 8 : 0);
-  const bool use_lds = mode == 3 && lds_l > 0 && lds_grid > 0 && cs.n4 / lds_l >= lds_grid &&
-                       64 * std::max(ldx, ldy) * 4 < (int64_t(1) << 32);
-  if (use_lds) {
-    const int nt = env_int("DOL_CSR_LDS_NT", 0);
-    auto go = [&](auto lc, auto ntc) {
-      constexpr int Lc = decltype(lc)::value;
-      constexpr bool NTc = decltype(ntc)::value;
-      auto kern = csr_lds_kernel<Lc, NTc, Epi>;
-      constexpr int lds = 2 * (kLdsImgBytes + 16 * Lc);  // two images, each with its zero row
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-      const int64_t n_slabs = cs.n4 / Lc;
-      hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(lds_grid)), dim3(kLdsT), lds, s, X, ldx,
-                         x_rows, Y, ldy, n_rows, n_slabs, rowptr, col, val, epi);
-      done4 = n_slabs * Lc;
-    };
-    using std::integral_constant;
-    using T = integral_constant<bool, true>;
-    using F = integral_constant<bool, false>;
-    switch (lds_l) {
-      case 8: nt ? go(integral_constant<int, 8>{}, T{}) : go(integral_constant<int, 8>{}, F{}); break;
-      case 4: nt ? go(integral_constant<int, 4>{}, T{}) : go(integral_constant<int, 4>{}, F{}); break;
-      case 2: nt ? go(integral_constant<int, 2>{}, T{}) : go(integral_constant<int, 2>{}, F{}); break;
-      default: nt ? go(integral_constant<int, 1>{}, T{}) : go(integral_constant<int, 1>{}, F{}); break;
-    }
-  }
-  const bool use_lds8 = !use_lds && mode == 5 && rows_max <= kLds8Rows && lds_grid > 0 && cs.n4 / 8 >= lds_grid &&
-                        64 * std::max(ldx, ldy) * 4 < (int64_t(1) << 32);
-  if (use_lds8) {
-    auto go = [&](auto ntc) {
-      auto kern = csr_lds8_kernel<decltype(ntc)::value, Epi>;
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                kLds8Bytes);
-      const int64_t n_slabs = cs.n4 / 8;
-      hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(lds_grid)), dim3(1024), kLds8Bytes, s, X, ldx, x_rows, Y,
-                         ldy, n_rows, n_slabs, rowptr, col, val, epi);
-      done4 = n_slabs * 8;
-    };
-    if (env_int("DOL_CSR_LDS_NT", 0)) go(std::integral_constant<bool, true>{});
-    else go(std::integral_constant<bool, false>{});
-  }
-  const bool use_lds2w = !use_lds && !use_lds8 && mode == 6 && rows_max <= 1024 && lds_grid > 0 &&
-                         cs.n4 / 4 >= 2 * lds_grid && 64 * std::max(ldx, ldy) * 4 < (int64_t(1) << 32);
-  if (use_lds2w) {
-    auto go = [&](auto ntc) {
-      auto kern = csr_lds2w_kernel<decltype(ntc)::value, Epi>;
-      constexpr int lds = (1024 + 1) * 64;
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-      const int64_t n_slabs = cs.n4 / 4;
-      hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(2 * lds_grid)), dim3(512), lds, s, X, ldx, x_rows, Y, ldy,
-                         n_rows, n_slabs, rowptr, col, val, epi);
-      done4 = n_slabs * 4;
-    };
-    if (env_int("DOL_CSR_LDS_NT", 0)) go(std::integral_constant<bool, true>{});
-    else go(std::integral_constant<bool, false>{});
-  }
-  const int tw = env_int("DOL_CSR_XCDP_TW", 8);
-  const bool use_xcdp = !use_lds && !use_lds8 && !use_lds2w && mode == 4 && lds_grid > 0 && cs.n4 >= 8 * tw;
-  if (use_xcdp) {
-    auto go = [&](auto twc, auto rptc) {
-      constexpr int TWc = decltype(twc)::value, RPTc = decltype(rptc)::value;
-      const int nw = lds_grid / 8;
-      const int rpw = static_cast<int>(cdiv(n_rows, nw));
-      if (rpw > RPTc * (1024 / TWc)) return false;
-      const int64_t nt = cs.n4 / TWc;
-      hipLaunchKernelGGL((csr_xcdp_kernel<TWc, RPTc, Epi>), dim3(static_cast<unsigned>(lds_grid)), dim3(1024), 0, s,
-                         X, ldx, Y, ldy, n_rows, rpw, nt, rowptr, col, val, epi);
-      done4 = nt * TWc;
-      return true;
-    };
-    using std::integral_constant;
-    bool ok = false;
-    if (int64_t(x_rows) * ldx / 4 >= (int64_t(1) << 32))
-      return fail(DOL_EINVAL, "%s: DOL_CSR_MODE=4: X too large for 32-bit row offsets", nm);
-    if (tw == 4) ok = go(integral_constant<int, 4>{}, integral_constant<int, 1>{});
-    else ok = go(integral_constant<int, 8>{}, integral_constant<int, 2>{});
-    if (!ok) return fail(DOL_EINVAL, "%s: DOL_CSR_MODE=4: too many rows per workgroup", nm);
-  }
-  const bool use_xcd = !use_lds && !use_lds8 && !use_lds2w && !use_xcdp && cs.n4 >= XW && (mode == 1 || (mode < 0 && n_rows >= 512));
+  const bool use_xcd = cs.n4 >= XW && (mode == 1 || (mode < 0 && n_rows >= 512));
   if (use_xcd) {
     const int passes = env_int("DOL_CSR_PASSES", XPASSES);
     auto go = [&](auto pc) {
@@ -1969,6 +1503,25 @@ int dol_stream_copy_f32(const float* src, float* dst, int64_t n, hipStream_t s) 
     hipLaunchKernelGGL(copy_scalar_kernel, dim3(2048), dim3(kThreads), 0, s, src, dst, n);
   }
   return check_launch("dol_stream_copy_f32");
+}
+
+int dol_stream_copy_rows_f32(const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t n_rows, int64_t P,
+                             hipStream_t s) {
+  const char* nm = "dol_stream_copy_rows_f32";
+  if (n_rows < 0 || P < 0) return fail(DOL_EINVAL, "%s: negative size", nm);
+  if (n_rows == 0 || P == 0) { g_err[0] = '\0'; return DOL_OK; }
+  if (!X || !Y) return fail(DOL_EINVAL, "%s: null pointer", nm);
+  if (ldx < P || ldy < P) return fail(DOL_EINVAL, "%s: ld < P", nm);
+  if (n_rows < 3 || !row_vec_ok(X, ldx) || !row_vec_ok(Y, ldy) || P % 4)
+    return fail(DOL_EINVAL, "%s: needs >= 3 rows, 16-B aligned rows and P %% 4 == 0", nm);
+  constexpr int R = 4;
+  const int64_t n4 = P / 4, nct = cdiv(n4, kThreads);
+  if (nct * cdiv(n_rows, R) > kMaxBlocks) return fail(DOL_EINVAL, "%s: too large", nm);
+  // the ring mix's launch with COPY: halo rows = the wrap-around neighbours, weights unused
+  const float* hp = X + int64_t(n_rows - 1) * ldx;
+  hipLaunchKernelGGL((ring_mix_dma_kernel<R, NoEpi, true, true>), dim3(static_cast<unsigned>(nct * cdiv(n_rows, R))),
+                     dim3(kThreads), 0, s, X, ldx, Y, ldy, n_rows, n4, nct, hp, X, X, X, NoEpi{});
+  return check_launch(nm);
 }
 
 }  // extern "C"

@@ -48,6 +48,7 @@ SIGNATURES = {
     "dol_ordered_mean_f32": [_ptr, _i64, _ptr, _i32, _i64, _ptr, _ptr],
     "dol_ordered_sum_f32": [_ptr, _i64, _ptr, _i32, _i64, _ptr, _ptr, _f32, _ptr],
     "dol_stream_copy_f32": [_ptr, _ptr, _i64, _ptr],
+    "dol_stream_copy_rows_f32": [_ptr, _i64, _ptr, _i64, _i32, _i64, _ptr],
     "dol_mlp_step_f32": [_ptr, _i64, _ptr, _i64, _ptr, _i64, _ptr, _ptr, _i64, _ptr, _i64, _i64, _ptr, _i64, _ptr,
                          _i32, _i32, _i32, _i32, _i32, _f32, _f32, _f32, ctypes.c_int, ctypes.c_int, _ptr, _ptr],
     "dol_mlp_step_workspace_bytes": [_i32, _i32, _i32],

@@ -18,7 +18,7 @@ __all__ = [
     "mix_ring_steps", "prox_admm_sgd", "admm_dual", "ordered_mean",
     "ordered_sum", "stream_copy", "dual_workspace_bytes", "prox_grad", "admm_step_dual", "mlp_step",
     "dgd_ring", "dgd_csr", "OBJECTIVES", "admm_ls_round", "admm_ls_round_workspace_bytes", "mix_csr_pm",
-    "transpose", "PM_MAX_AGENTS",
+    "transpose", "PM_MAX_AGENTS", "stream_copy_rows",
 ]
 
 PM_MAX_AGENTS = 8192  # dol_mix_csr_pm_f32: one p-row image (<= 32 KiB) per LDS stage
@@ -532,6 +532,17 @@ def stream_copy(src: torch.Tensor, dst: torch.Tensor) -> torch.Tensor:
         raise ValueError("stream_copy: contiguous tensors of equal size required")
     _native.call("dol_stream_copy_f32", src.data_ptr(), dst.data_ptr(), src.numel(), _stream(src))
     return dst
+
+
+def stream_copy_rows(X: torch.Tensor, Y: torch.Tensor, P: Optional[int] = None) -> torch.Tensor:
+    """Y[:, :P] = X[:, :P] in the ring mix's tile geometry (roofline calibration)."""
+    P = X.shape[1] if P is None else P
+    ldx = _check_rows("X", X, P)
+    ldy = _check_rows("Y", Y, P)
+    if Y.shape[0] < X.shape[0]:
+        raise ValueError("Y has fewer rows than X")
+    _native.call("dol_stream_copy_rows_f32", X.data_ptr(), ldx, Y.data_ptr(), ldy, X.shape[0], P, _stream(X))
+    return Y
 
 
 def mlp_step(w: torch.Tensor, X: torch.Tensor, y: torch.Tensor, d: int, h: int, c: int,

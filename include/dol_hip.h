@@ -329,6 +329,14 @@ int dol_er_stochastic_f32(float* W, int64_t ldw, int32_t n, float p, uint64_t se
 /* Streaming copy dst = src (n floats): HBM calibration kernel for roofline. */
 int dol_stream_copy_f32(const float* src, float* dst, int64_t n, hipStream_t s);
 
+/* Y[:, :P] = X[:, :P] by the ring mix's own kernel with the stencil replaced by
+ * the tile's row (same launch, loads incl. halo rows, cache policies and
+ * stores): the HBM ceiling of exactly that access pattern, the roofline's
+ * second calibration (bytes = 2 * n_rows * P * 4, as the mix).  >= 3 rows,
+ * 16-B aligned rows, P % 4 == 0. */
+int dol_stream_copy_rows_f32(const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t n_rows, int64_t P,
+                             hipStream_t s);
+
 #ifdef __cplusplus
 }
 #endif

@@ -47,14 +47,16 @@ def mixing_round(W: torch.Tensor, agents: List[Agent]) -> None:
             ag.state[k].copy_(v)
 
 
-def time_rounds(W: torch.Tensor, X: torch.Tensor, min_seconds: float = 10.0, max_rounds: int = 50):
+def time_rounds(W: torch.Tensor, X: torch.Tensor, min_seconds: float = 10.0, max_rounds: int = 50,
+                warmup: bool = True):
     """Run rounds on agents whose parameters are rows of X until min_seconds
-    have elapsed (at least 2 rounds).  Returns (rounds, seconds)."""
+    have elapsed (at least min(2, max_rounds) rounds).  Returns (rounds, seconds)."""
     agents = [Agent({"w": X[i]}) for i in range(X.shape[0])]
-    mixing_round(W, agents)  # warm-up (allocator, thread pool)
+    if warmup:
+        mixing_round(W, agents)  # allocator, thread pool
     t0 = time.perf_counter()
     r = 0
-    while r < 2 or (time.perf_counter() - t0 < min_seconds and r < max_rounds):
+    while r < min(2, max_rounds) or (time.perf_counter() - t0 < min_seconds and r < max_rounds):
         mixing_round(W, agents)
         r += 1
     return r, time.perf_counter() - t0

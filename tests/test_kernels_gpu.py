@@ -639,3 +639,16 @@ def test_erdos_renyi_device_plan_within_gamma_bound(gpu):
     csr = G.csr_from_dense(Wc)
     exact = oracle.mix_csr(X, csr.rowptr, csr.col, csr.val)
     assert np.all(np.abs(Y.cpu().numpy() - exact) <= 2 * _gamma_bound(Wc, X) + 1e-30)
+
+
+def test_stream_copy_rows_is_a_copy(gpu):
+    """The roofline calibration copy (the ring kernel with the stencil replaced
+    by the row itself) reproduces X exactly, including the last partial tile."""
+    X = torch.randn(11, 4096 + 64, device=gpu)
+    Y = torch.full_like(X, 3.0)
+    ops.stream_copy_rows(X, Y, P=4096)
+    torch.cuda.synchronize()
+    assert torch.equal(Y[:, :4096], X[:, :4096])
+    assert (Y[:, 4096:] == 3.0).all()
+    with pytest.raises(ops.DolNativeError):
+        ops.stream_copy_rows(X, Y, P=4095)
