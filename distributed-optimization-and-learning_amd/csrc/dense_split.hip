@@ -398,7 +398,7 @@ inline bool fused_x_ok(const float* X, int64_t ldx, int64_t P, int flags) {
 }  // namespace
 
 extern "C" int64_t dol_mix_dense_split3_workspace_bytes(int32_t M, int32_t K, int64_t P, int flags) {
-  if (M <= 0 || K <= 0 || P <= 0) return 0;
+  if (M <= 0 || K <= 0 || P <= 0 || P > dol::kMaxDim) return 0;
   const Split3Geom g = geom(M, K, P);
   // FUSE_X + X_ROWS_PADDED promise the fused path (given an aligned X): W pieces only
   const bool fused = (flags & DOL_SPLIT3_FUSE_X) && (flags & DOL_SPLIT3_X_ROWS_PADDED) && P >= 4;
@@ -408,6 +408,7 @@ extern "C" int64_t dol_mix_dense_split3_workspace_bytes(int32_t M, int32_t K, in
 extern "C" int dol_mix_dense_split3_f32(const float* W, int64_t ldw, const float* X, int64_t ldx, float* Y,
                                         int64_t ldy, int32_t M, int32_t K, int64_t P, void* work,
                                         int64_t work_bytes, int flags, hipStream_t s) {
+  DOL_DIMS_OK("dol_mix_dense_split3_f32", ldw, ldx, ldy, P, work_bytes);
   using dol::fail;
   if (M < 0 || K < 0 || P < 0) return fail(DOL_EINVAL, "dol_mix_dense_split3_f32: negative size");
   if (M == 0 || P == 0) return DOL_OK;

@@ -1,10 +1,24 @@
 // dol_common.h — error plumbing shared by the translation units of libdol_hip.so.
 #pragma once
 
+#include <stdint.h>
+
 namespace dol {
+// Every size / leading dimension an entry point accepts is at most 2^40
+// elements (4 TiB of fp32, far above one GPU's 288 GB), so no byte or block
+// count derived from them can overflow int64 (checked under UBSan,
+// tests/test_native_abi.py).
+constexpr int64_t kMaxDim = int64_t(1) << 40;
 extern thread_local char g_err[512];
 // Format the thread-local error message and return `code`.
 int fail(int code, const char* fmt, ...);
 // DOL_OK, or -(hipError_t) of a failed launch (message set).
 int check_launch(const char* what);
 }  // namespace dol
+
+// First statement of an entry point: reject sizes above kMaxDim.
+#define DOL_DIMS_OK(nm, ...)                                                          \
+  do {                                                                                \
+    for (const int64_t dol_v_ : {__VA_ARGS__})                                        \
+      if (dol_v_ > dol::kMaxDim) return dol::fail(DOL_EINVAL, "%s: size above 2^40 elements", nm); \
+  } while (0)

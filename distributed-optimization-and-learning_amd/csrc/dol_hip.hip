@@ -924,7 +924,12 @@ __global__ __launch_bounds__(256, 1) void dense_mix_mfma_kernel(
 // ----------------------------------------------------------------------------
 // host-side launch helpers
 // ----------------------------------------------------------------------------
-inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+inline int64_t cdiv(int64_t a, int64_t b) { return a / b + (a % b != 0); }
+// a * b saturated at INT64_MAX: block-count checks of absurd sizes must fail, not overflow
+inline int64_t mul_sat(int64_t a, int64_t b) {
+  int64_t r;
+  return __builtin_mul_overflow(a, b, &r) ? INT64_MAX : r;
+}
 
 // Split [0, P) into a f4 part and a scalar tail; returns whether the
 // f4 path is legal for all given (base, ld) pairs.
@@ -1046,7 +1051,7 @@ int mix_csr_impl(const char* nm, const float* X, int64_t ldx, int32_t x_rows, fl
   constexpr int XW = 32, XPASSES = 2;  // XCD-pinned tiles: 512 B of a row, 16 rows per block
   // 0 = 4 KiB tiles, 1 = XCD-pinned (DOL_CSR_MODE; default: XCD-pinned from 512 rows)
   const int mode = env_int("DOL_CSR_MODE", -1);
-  if (cdiv(cs.n4, kThreads) * cdiv(n_rows, RPB) > kMaxBlocks)
+  if (mul_sat(cdiv(cs.n4, kThreads), cdiv(n_rows, RPB)) > kMaxBlocks)
     return fail(DOL_EINVAL, "%s: problem too large for one launch", nm);
   int64_t done4 = 0;
   const bool use_xcd = cs.n4 >= XW && (mode == 1 || (mode < 0 && n_rows >= 512));
@@ -1101,7 +1106,7 @@ int mix_ring_impl(const char* nm, const float* X, int64_t ldx, float* Y, int64_t
     if constexpr (kPlain) dma = env_int("DOL_RING_DMA", 1) != 0;
     if (dma) {
       constexpr int R = 4;
-      if (nct * cdiv(n_rows, R) > kMaxBlocks) return fail(DOL_EINVAL, "%s: problem too large for one launch", nm);
+      if (mul_sat(nct, cdiv(n_rows, R)) > kMaxBlocks) return fail(DOL_EINVAL, "%s: problem too large for one launch", nm);
       if (env_int("DOL_RING_NTI", 1))
         hipLaunchKernelGGL((ring_mix_dma_kernel<R, Epi, true>), dim3(static_cast<unsigned>(nct * cdiv(n_rows, R))),
                            dim3(kThreads), 0, s, X, ldx, Y, ldy, n_rows, cs.n4, nct, halo_prev, halo_next, w_prev, w_next, epi);
@@ -1112,13 +1117,13 @@ int mix_ring_impl(const char* nm, const float* X, int64_t ldx, float* Y, int64_t
       const int pf = env_int("DOL_RING_PF", 4);
       const int nt = env_int("DOL_RING_NT", 2);
       const int rpb = ring_rows_per_block(n_rows, nct, pf);
-      if (nct * cdiv(n_rows, rpb) > kMaxBlocks) return fail(DOL_EINVAL, "%s: problem too large for one launch", nm);
+      if (mul_sat(nct, cdiv(n_rows, rpb)) > kMaxBlocks) return fail(DOL_EINVAL, "%s: problem too large for one launch", nm);
       launch_ring_variant<f4>(pf, nt, X, ldx, Y, ldy, n_rows, 0, cs.n4, rpb, halo_prev, halo_next, w_prev, w_next, s);
     }
   }
   if (cs.tail > 0) {
     const int rpb = ring_rows_per_block(n_rows, cdiv(cs.tail, kThreads), 4);
-    if (cdiv(cs.tail, kThreads) * cdiv(n_rows, rpb) > kMaxBlocks)
+    if (mul_sat(cdiv(cs.tail, kThreads), cdiv(n_rows, rpb)) > kMaxBlocks)
       return fail(DOL_EINVAL, "%s: problem too large for one launch", nm);
     launch_ring<float, 4, false, true, Epi>(X, ldx, Y, ldy, n_rows, cs.n4 * 4, cs.tail, rpb, halo_prev, halo_next,
                                             w_prev, w_next, s, epi);
@@ -1140,12 +1145,14 @@ const char* dol_last_error(void) { return g_err; }
 int dol_mix_csr_f32(const float* X, int64_t ldx, int32_t x_rows, float* Y, int64_t ldy,
                     int32_t n_rows, int64_t P, const int32_t* rowptr, const int32_t* col,
                     const float* val, hipStream_t s) {
+  DOL_DIMS_OK("dol_mix_csr_f32", ldx, ldy, P);
   return mix_csr_impl("dol_mix_csr_f32", X, ldx, x_rows, Y, ldy, n_rows, P, rowptr, col, val, NoEpi{}, true, s);
 }
 
 int dol_mix_ring_f32(const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t n_rows, int64_t P,
                      const float* halo_prev, const float* halo_next, const float* w_prev,
                      const float* w_next, hipStream_t s) {
+  DOL_DIMS_OK("dol_mix_ring_f32", ldx, ldy, P);
   return mix_ring_impl("dol_mix_ring_f32", X, ldx, Y, ldy, n_rows, P, halo_prev, halo_next, w_prev, w_next,
                        NoEpi{}, true, s);
 }
@@ -1193,6 +1200,7 @@ int dol_dgd_ring_f32(const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t
                      const float* halo_prev, const float* halo_next, const float* w_prev, const float* w_next,
                      const float* target, int64_t ldt, float* mom, int64_t ldm, int32_t objective,
                      int32_t local_steps, float lr, float momentum, int first_step, hipStream_t s) {
+  DOL_DIMS_OK("dol_dgd_ring_f32", ldx, ldy, P, ldt, ldm);
   const char* nm = "dol_dgd_ring_f32";
   const DgdArgs d{target, ldt, mom, ldm, objective, local_steps, lr, momentum, first_step};
   bool evec = false;
@@ -1210,6 +1218,7 @@ int dol_dgd_csr_f32(const float* X, int64_t ldx, int32_t x_rows, float* Y, int64
                     const int32_t* rowptr, const int32_t* col, const float* val, const float* target, int64_t ldt,
                     float* mom, int64_t ldm, int32_t objective, int32_t local_steps, float lr, float momentum,
                     int first_step, hipStream_t s) {
+  DOL_DIMS_OK("dol_dgd_csr_f32", ldx, ldy, P, ldt, ldm);
   const char* nm = "dol_dgd_csr_f32";
   const DgdArgs d{target, ldt, mom, ldm, objective, local_steps, lr, momentum, first_step};
   bool evec = false;
@@ -1225,6 +1234,7 @@ int dol_dgd_csr_f32(const float* X, int64_t ldx, int32_t x_rows, float* Y, int64
 
 int dol_mix_dense_f32(const float* W, int64_t ldw, const float* X, int64_t ldx, float* Y, int64_t ldy,
                       int32_t M, int32_t K, int64_t P, hipStream_t s) {
+  DOL_DIMS_OK("dol_mix_dense_f32", ldw, ldx, ldy, P);
   if (M < 0 || K < 0 || P < 0) return fail(DOL_EINVAL, "dol_mix_dense_f32: negative size");
   if (M == 0 || P == 0) { g_err[0] = '\0'; return DOL_OK; }
   if (!W || !X || !Y) return fail(DOL_EINVAL, "dol_mix_dense_f32: null pointer");
@@ -1246,6 +1256,7 @@ int dol_mix_dense_f32(const float* W, int64_t ldw, const float* X, int64_t ldx, 
 int dol_mix_ring_steps_f32(const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t n_rows,
                            int64_t P, int32_t steps, const float* w_prev, const float* w_next,
                            hipStream_t s) {
+  DOL_DIMS_OK("dol_mix_ring_steps_f32", ldx, ldy, P);
   if (n_rows < 0 || P < 0 || steps < 0) return fail(DOL_EINVAL, "dol_mix_ring_steps_f32: negative size");
   if (n_rows == 0 || P == 0) { g_err[0] = '\0'; return DOL_OK; }
   if (!X || !Y || !w_prev || !w_next) return fail(DOL_EINVAL, "dol_mix_ring_steps_f32: null pointer");
@@ -1288,6 +1299,7 @@ int dol_prox_admm_sgd_f32(float* w, int64_t ldw, float* buf, int64_t ldb, float*
                           const float* theta, const float* alpha, int64_t lda, float rho, float lr,
                           float momentum, int first_step, int write_grad, int32_t n_agents,
                           int64_t P, hipStream_t s) {
+  DOL_DIMS_OK("dol_prox_admm_sgd_f32", ldw, ldb, ldg, lda, P);
   if (n_agents < 0 || P < 0) return fail(DOL_EINVAL, "dol_prox_admm_sgd_f32: negative size");
   if (n_agents == 0 || P == 0) { g_err[0] = '\0'; return DOL_OK; }
   if (!w || !g) return fail(DOL_EINVAL, "dol_prox_admm_sgd_f32: null w or g");
@@ -1299,7 +1311,7 @@ int dol_prox_admm_sgd_f32(float* w, int64_t ldw, float* buf, int64_t ldb, float*
   const bool vec_ok = row_vec_ok(w, ldw) && row_vec_ok(g, ldg) && (mode == 0 || row_vec_ok(buf, ldb)) &&
                       row_vec_ok(theta, 0) && row_vec_ok(alpha, alpha ? lda : 0);
   const ColSplit cs = split_cols(P, vec_ok);
-  if (cdiv(cs.n4 + cs.tail, kThreads) * n_agents > kMaxBlocks)
+  if (mul_sat(cdiv(cs.n4 + cs.tail, kThreads), n_agents) > kMaxBlocks)
     return fail(DOL_EINVAL, "dol_prox_admm_sgd_f32: problem too large for one launch");
   const bool th = theta != nullptr, al = alpha != nullptr, wg = write_grad != 0;
   if (cs.n4 > 0)
@@ -1315,6 +1327,7 @@ int dol_admm_step_dual_f32(float* w, int64_t ldw, float* buf, int64_t ldb, float
                            const float* theta, float* alpha, int64_t lda, float rho, float lr,
                            float momentum, int first_step, int write_grad, int32_t n_agents, int64_t P,
                            hipStream_t s) {
+  DOL_DIMS_OK("dol_admm_step_dual_f32", ldw, ldb, ldg, lda, P);
   if (n_agents < 0 || P < 0) return fail(DOL_EINVAL, "dol_admm_step_dual_f32: negative size");
   if (n_agents == 0 || P == 0) { g_err[0] = '\0'; return DOL_OK; }
   if (!w || !g || !theta || !alpha) return fail(DOL_EINVAL, "dol_admm_step_dual_f32: null pointer");
@@ -1324,7 +1337,7 @@ int dol_admm_step_dual_f32(float* w, int64_t ldw, float* buf, int64_t ldb, float
   const bool vec_ok = row_vec_ok(w, ldw) && row_vec_ok(g, ldg) && (mode == 0 || row_vec_ok(buf, ldb)) &&
                       row_vec_ok(theta, 0) && row_vec_ok(alpha, lda);
   const ColSplit cs = split_cols(P, vec_ok);
-  if (cdiv(cs.n4 + cs.tail, kThreads) * n_agents > kMaxBlocks) return fail(DOL_EINVAL, "dol_admm_step_dual_f32: too large");
+  if (mul_sat(cdiv(cs.n4 + cs.tail, kThreads), n_agents) > kMaxBlocks) return fail(DOL_EINVAL, "dol_admm_step_dual_f32: too large");
   auto launch = [&](auto vtag, auto mode_c, auto wg_c, int64_t c_off, int64_t nc) {
     using V = decltype(vtag);
     constexpr int M = decltype(mode_c)::value;
@@ -1349,6 +1362,7 @@ int dol_admm_step_dual_f32(float* w, int64_t ldw, float* buf, int64_t ldb, float
 int dol_prox_grad_f32(float* g, int64_t ldg, const float* w, int64_t ldw, const float* theta,
                       const float* alpha, int64_t lda, float rho, int32_t n_agents, int64_t P,
                       hipStream_t s) {
+  DOL_DIMS_OK("dol_prox_grad_f32", ldg, ldw, lda, P);
   if (n_agents < 0 || P < 0) return fail(DOL_EINVAL, "dol_prox_grad_f32: negative size");
   if (n_agents == 0 || P == 0) { g_err[0] = '\0'; return DOL_OK; }
   if (!g || !w || !theta) return fail(DOL_EINVAL, "dol_prox_grad_f32: null pointer");
@@ -1363,14 +1377,14 @@ int dol_prox_grad_f32(float* g, int64_t ldg, const float* w, int64_t ldw, const 
     if (alpha) hipLaunchKernelGGL((prox_grad_kernel<V, true>), grid, dim3(kThreads), 0, s, g, ldg, w, ldw, theta, alpha, lda, rho, c_off, nc, nct);
     else hipLaunchKernelGGL((prox_grad_kernel<V, false>), grid, dim3(kThreads), 0, s, g, ldg, w, ldw, theta, alpha, lda, rho, c_off, nc, nct);
   };
-  if (cdiv(cs.n4 + cs.tail, kThreads) * n_agents > kMaxBlocks) return fail(DOL_EINVAL, "dol_prox_grad_f32: too large");
+  if (mul_sat(cdiv(cs.n4 + cs.tail, kThreads), n_agents) > kMaxBlocks) return fail(DOL_EINVAL, "dol_prox_grad_f32: too large");
   if (cs.n4 > 0) launch(f4{}, 0, cs.n4);
   if (cs.tail > 0) launch(float{}, cs.n4 * 4, cs.tail);
   return check_launch("dol_prox_grad_f32");
 }
 
 int64_t dol_admm_dual_workspace_bytes(int32_t n_agents, int64_t P) {
-  if (n_agents <= 0 || P <= 0) return 0;
+  if (n_agents <= 0 || P <= 0 || P > dol::kMaxDim) return 0;
   // the scalar path has the most chunks: cdiv(P, kThreads*kDualIters)
   return int64_t(n_agents) * cdiv(P, int64_t(kThreads) * kDualIters) * int64_t(sizeof(double));
 }
@@ -1378,6 +1392,7 @@ int64_t dol_admm_dual_workspace_bytes(int32_t n_agents, int64_t P) {
 int dol_admm_dual_f32(float* alpha, int64_t lda, const float* w, int64_t ldw, const float* theta,
                       float rho, int32_t n_agents, int64_t P, double* resid_sq, void* work,
                       hipStream_t s) {
+  DOL_DIMS_OK("dol_admm_dual_f32", lda, ldw, P);
   if (n_agents < 0 || P < 0) return fail(DOL_EINVAL, "dol_admm_dual_f32: negative size");
   if (n_agents == 0) { g_err[0] = '\0'; return DOL_OK; }
   if (P > 0 && (!alpha || !w || !theta)) return fail(DOL_EINVAL, "dol_admm_dual_f32: null pointer");
@@ -1390,7 +1405,7 @@ int dol_admm_dual_f32(float* alpha, int64_t lda, const float* w, int64_t ldw, co
   const bool vec = row_vec_ok(alpha, lda) && row_vec_ok(w, ldw) && row_vec_ok(theta, 0);
   const int64_t per_block = int64_t(kThreads) * kDualIters;
   const int64_t chunks = vec ? std::max<int64_t>(1, cdiv(P / 4, per_block)) : cdiv(P, per_block);
-  if (chunks * n_agents > kMaxBlocks) return fail(DOL_EINVAL, "dol_admm_dual_f32: problem too large");
+  if (mul_sat(chunks, n_agents) > kMaxBlocks) return fail(DOL_EINVAL, "dol_admm_dual_f32: problem too large");
   double* partial = static_cast<double*>(work);
   const dim3 grid(static_cast<unsigned>(chunks * n_agents));
   if (resid_sq) {
@@ -1405,7 +1420,7 @@ int dol_admm_dual_f32(float* alpha, int64_t lda, const float* w, int64_t ldw, co
 }
 
 int64_t dol_admm_ls_round_workspace_bytes(int32_t m, int64_t P) {
-  if (m <= 0 || P <= 0) return 0;
+  if (m <= 0 || P <= 0 || P > dol::kMaxDim) return 0;
   return 2 * dol_admm_dual_workspace_bytes(m, P);  // ||w - theta||^2 and ||alpha||^2 partials
 }
 
@@ -1413,6 +1428,7 @@ int dol_admm_ls_round_f32(float* w, int64_t ldw, float* buf, int64_t ldb, float*
                           const float* target, int64_t ldt, const float* theta, const int32_t* agents,
                           const int32_t* first, int32_t m, int64_t P, float rho, float lr, float momentum,
                           int32_t local_steps, double* resid_sq, double* alpha_sq, void* work, hipStream_t s) {
+  DOL_DIMS_OK("dol_admm_ls_round_f32", ldw, ldb, lda, ldt, P);
   const char* nm = "dol_admm_ls_round_f32";
   if (m < 0 || P < 0 || local_steps < 0) return fail(DOL_EINVAL, "%s: negative size", nm);
   if (m == 0) { g_err[0] = '\0'; return DOL_OK; }
@@ -1432,7 +1448,7 @@ int dol_admm_ls_round_f32(float* w, int64_t ldw, float* buf, int64_t ldb, float*
                    (!mom || row_vec_ok(buf, ldb));
   const int64_t per_block = int64_t(kThreads) * kDualIters;
   const int64_t chunks = vec ? std::max<int64_t>(1, cdiv(P / 4, per_block)) : cdiv(P, per_block);
-  if (chunks * m > kMaxBlocks) return fail(DOL_EINVAL, "%s: problem too large", nm);
+  if (mul_sat(chunks, m) > kMaxBlocks) return fail(DOL_EINVAL, "%s: problem too large", nm);
   double* partial = static_cast<double*>(work);
   const dim3 grid(static_cast<unsigned>(chunks * m));
   auto go = [&](auto vc, auto mc, auto rc) {
@@ -1460,6 +1476,7 @@ int dol_admm_ls_round_f32(float* w, int64_t ldw, float* buf, int64_t ldb, float*
 
 int dol_ordered_sum_f32(const float* W, int64_t ldw, const int32_t* order, int32_t m, int64_t P,
                         const float* acc_in, float* acc_out, float scale, hipStream_t s) {
+  DOL_DIMS_OK("dol_ordered_sum_f32", ldw, P);
   if (m < 0 || P < 0) return fail(DOL_EINVAL, "dol_ordered_sum_f32: negative size");
   if (P == 0) { g_err[0] = '\0'; return DOL_OK; }
   if (m == 0 && !acc_in) return fail(DOL_EINVAL, "dol_ordered_sum_f32: m == 0 needs acc_in");
@@ -1480,12 +1497,14 @@ int dol_ordered_sum_f32(const float* W, int64_t ldw, const int32_t* order, int32
 
 int dol_ordered_mean_f32(const float* W, int64_t ldw, const int32_t* order, int32_t m, int64_t P,
                          float* theta, hipStream_t s) {
+  DOL_DIMS_OK("dol_ordered_mean_f32", ldw, P);
   if (m <= 0) return fail(DOL_EINVAL, "dol_ordered_mean_f32: m must be >= 1 (reference indexes w[0])");
   if (theta == W) return fail(DOL_EINVAL, "dol_ordered_mean_f32: theta aliases W");
   return dol_ordered_sum_f32(W, ldw, order, m, P, nullptr, theta, static_cast<float>(m), s);
 }
 
 int dol_stream_copy_f32(const float* src, float* dst, int64_t n, hipStream_t s) {
+  DOL_DIMS_OK("dol_stream_copy_f32", n);
   if (n < 0) return fail(DOL_EINVAL, "dol_stream_copy_f32: negative size");
   if (n == 0) { g_err[0] = '\0'; return DOL_OK; }
   if (!src || !dst) return fail(DOL_EINVAL, "dol_stream_copy_f32: null pointer");
@@ -1507,6 +1526,7 @@ int dol_stream_copy_f32(const float* src, float* dst, int64_t n, hipStream_t s) 
 
 int dol_stream_copy_rows_f32(const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t n_rows, int64_t P,
                              hipStream_t s) {
+  DOL_DIMS_OK("dol_stream_copy_rows_f32", ldx, ldy, P);
   const char* nm = "dol_stream_copy_rows_f32";
   if (n_rows < 0 || P < 0) return fail(DOL_EINVAL, "%s: negative size", nm);
   if (n_rows == 0 || P == 0) { g_err[0] = '\0'; return DOL_OK; }
@@ -1516,7 +1536,7 @@ int dol_stream_copy_rows_f32(const float* X, int64_t ldx, float* Y, int64_t ldy,
     return fail(DOL_EINVAL, "%s: needs >= 3 rows, 16-B aligned rows and P %% 4 == 0", nm);
   constexpr int R = 4;
   const int64_t n4 = P / 4, nct = cdiv(n4, kThreads);
-  if (nct * cdiv(n_rows, R) > kMaxBlocks) return fail(DOL_EINVAL, "%s: too large", nm);
+  if (mul_sat(nct, cdiv(n_rows, R)) > kMaxBlocks) return fail(DOL_EINVAL, "%s: too large", nm);
   // the ring mix's launch with COPY: halo rows = the wrap-around neighbours, weights unused
   const float* hp = X + int64_t(n_rows - 1) * ldx;
   hipLaunchKernelGGL((ring_mix_dma_kernel<R, NoEpi, true, true>), dim3(static_cast<unsigned>(nct * cdiv(n_rows, R))),

@@ -78,6 +78,7 @@ __global__ __launch_bounds__(kThreads) void er_stochastic_kernel(float* __restri
 }  // namespace
 
 extern "C" int dol_er_stochastic_f32(float* W, int64_t ldw, int32_t n, float p, uint64_t seed, hipStream_t s) {
+  DOL_DIMS_OK("dol_er_stochastic_f32", ldw);
   using dol::fail;
   if (n < 0) return fail(DOL_EINVAL, "dol_er_stochastic_f32: negative size");
   if (n == 0) return DOL_OK;

@@ -468,11 +468,12 @@ __global__ __launch_bounds__(kThreads) void mlp_dw1_kernel(MlpArgs a, const floa
 }  // namespace
 
 extern "C" int64_t dol_mlp_step_workspace_bytes(int32_t n_agents, int32_t B, int32_t h) {
-  if (n_agents <= 0 || B <= 0 || h <= 0) return 0;
+  if (n_agents <= 0 || B <= 0 || h <= 0 || B > kMaxB || h > kMaxH) return 0;  // outside the step's limits
   return int64_t(n_agents) * B * h * int64_t(sizeof(float));
 }
 
 extern "C" int64_t dol_mlp_step_lds_bytes(int32_t B, int32_t h, int32_t c) {
+  if (B <= 0 || h <= 0 || c <= 0 || B > kMaxB || h > kMaxH || c > kMaxC) return 0;  // outside the step's limits
   return sizeof(float) * (fwd_union_floats(B, h, c) + h + c + B) + sizeof(int) * int64_t(B);
 }
 
@@ -482,6 +483,7 @@ extern "C" int dol_mlp_step_f32(float* w, int64_t ldw, float* grad, int64_t ldg,
                                 float* loss, int32_t n_agents, int32_t B, int32_t d, int32_t h, int32_t c,
                                 float lr, float momentum, float rho, int first_step, int update,
                                 void* work, hipStream_t s) {
+  DOL_DIMS_OK("dol_mlp_step_f32", ldw, ldg, ldm, lda, ldx_agent, ldx_row, ldy_agent);
   using dol::fail;
   if (n_agents < 0) return fail(DOL_EINVAL, "dol_mlp_step_f32: negative agent count");
   if (n_agents == 0) { dol::g_err[0] = '\0'; return DOL_OK; }

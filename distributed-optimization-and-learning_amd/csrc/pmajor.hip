@@ -292,6 +292,7 @@ extern "C" {
 
 int dol_mix_csr_pm_f32(const float* XT, int64_t ldx, int32_t x_rows, float* YT, int64_t ldy, int32_t n_rows,
                        int64_t P, const int32_t* rowptr, const int32_t* col, const float* val, hipStream_t s) {
+  DOL_DIMS_OK("dol_mix_csr_pm_f32", ldx, ldy, P);
   const char* nm = "dol_mix_csr_pm_f32";
   if (n_rows < 0 || x_rows < 0 || P < 0) return fail(DOL_EINVAL, "%s: negative size", nm);
   if (n_rows == 0 || P == 0) { dol::g_err[0] = '\0'; return DOL_OK; }
@@ -356,6 +357,7 @@ int dol_mix_csr_pm_f32(const float* XT, int64_t ldx, int32_t x_rows, float* YT, 
 }
 
 int dol_transpose_f32(const float* A, int64_t lda, float* B, int64_t ldb, int64_t rows, int64_t cols, hipStream_t s) {
+  DOL_DIMS_OK("dol_transpose_f32", lda, ldb, rows, cols);
   const char* nm = "dol_transpose_f32";
   if (rows < 0 || cols < 0) return fail(DOL_EINVAL, "%s: negative size", nm);
   if (rows == 0 || cols == 0) { dol::g_err[0] = '\0'; return DOL_OK; }

@@ -76,3 +76,32 @@ def test_cpu_tensors_are_refused():
         ops.mix_ring(x, torch.zeros(4, 8), torch.ones(4), torch.ones(4))
     with pytest.raises(_native.DolNativeError):
         ops.prox_admm_sgd(x, torch.zeros(4, 8), lr=0.1)
+
+
+def _asan_runtime():
+    import glob
+    hits = sorted(glob.glob("/opt/rocm/lib/llvm/lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so"))
+    return hits[-1] if hits else None
+
+
+def test_argument_validation_under_asan_ubsan():
+    """SURVEY §5 sanitizer row: the host side of the C-ABI built with
+    -fsanitize=address,undefined (csrc/Makefile `asan`; device code unchanged)
+    rejects NULL / negative / overflowing / misaligned arguments of every entry
+    point without a sanitizer report (tests/asan_abi_driver.py, in a subprocess
+    with the ASan runtime preloaded)."""
+    import subprocess
+    import sys
+    rt = _asan_runtime()
+    if rt is None:
+        pytest.skip("no clang ASan runtime in this image")
+    lib = os.path.join(os.path.dirname(_native.LIB_PATH), "libdol_hip_asan.so")
+    if not os.path.exists(lib):
+        subprocess.run(["make", "-s", "-C", _native.CSRC, "asan"], check=True, capture_output=True)
+    env = dict(os.environ, LD_PRELOAD=rt, ASAN_OPTIONS="detect_leaks=0:verify_asan_link_order=0",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1", HIP_VISIBLE_DEVICES="")
+    here = os.path.dirname(os.path.abspath(__file__))
+    r = subprocess.run([sys.executable, os.path.join(here, "asan_abi_driver.py"), lib, _native.PKG_ROOT],
+                       env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    assert "asan-abi ok" in r.stdout
