@@ -40,12 +40,12 @@ def flat(sd):
     return torch.cat([v.detach().reshape(-1).float().cpu() for v in sd.values()]).numpy()
 
 
-def summary(vec):
-    return {"sample": vec[::STRIDE].tolist(), "l2": float(np.linalg.norm(vec.astype(np.float64))),
+def summary(vec, stride=STRIDE):
+    return {"sample": vec[::stride].tolist(), "l2": float(np.linalg.norm(vec.astype(np.float64))),
             "sum": float(vec.astype(np.float64).sum())}
 
 
-def run_dist(cls_name="DecFedAvg", overrides=None, eps=None):
+def run_dist(cls_name="DecFedAvg", overrides=None, eps=None, stride=STRIDE):
     mods = _import_project(DIST_SRC, ["utils", "sampling", "simulators"])
     U, S, sim = mods["utils"], mods["sampling"], mods["simulators"]
 
@@ -62,7 +62,7 @@ def run_dist(cls_name="DecFedAvg", overrides=None, eps=None):
             s.run(args.rounds)
         else:
             s.run(args.rounds, eps)
-    return {"history": s.history, "agents": [summary(flat(c.model.state_dict())) for c in s.clients]}
+    return {"history": s.history, "agents": [summary(flat(c.model.state_dict()), stride) for c in s.clients]}
 
 
 # further gossip runs: other topologies / modes, and the other simulator classes
@@ -78,7 +78,7 @@ DIST_VARIANTS = {
 }
 
 
-def run_dec(server_name):
+def run_dec(server_name, overrides=None, frac=FRAC, rounds=ROUNDS, stride=STRIDE):
     mods = _import_project(DEC_SRC, ["utils", "sampling", "servers"])
     U, S, srv = mods["utils"], mods["sampling"], mods["servers"]
 
@@ -88,16 +88,33 @@ def run_dec(server_name):
         return train, test, groups
 
     srv.get_dataset = get_dataset
-    args = U.DotDict(dict(DEC_ARGS, device="cpu"))
+    args = U.DotDict(dict(DEC_ARGS, **(overrides or {}), device="cpu"))
     with contextlib.redirect_stdout(io.StringIO()):
         s = getattr(srv, server_name)(args)
-        s.run(FRAC, ROUNDS)
+        s.run(frac, rounds)
     out = {"history": [{k: float(v) for k, v in h.items()} for h in s.history],
-           "global": summary(flat(s.global_client.model.state_dict())),
-           "clients": [summary(flat(c.model.state_dict())) for c in s.clients]}
+           "global": summary(flat(s.global_client.model.state_dict()), stride),
+           "clients": [summary(flat(c.model.state_dict()), stride) for c in s.clients]}
     if server_name == "FedAdmm_Server":
-        out["alpha"] = [summary(flat(c.alpha)) for c in s.clients]
+        out["alpha"] = [summary(flat(c.alpha), stride) for c in s.clients]
     return out
+
+
+# The notebooks' own argument cells (PD.ipynb cell[8] with Server.run(0.1, .) in
+# cells 12-23; WA.ipynb cell[11]): configs 1 and 2 at their shipped shapes, on
+# synthetic MNIST-shaped data sized so each client holds 54 (PD) / 180 (WA)
+# training samples, 2 rounds.  A coarser parameter sample (every 49999th).
+NB_STRIDE = 49999
+DEC_NOTEBOOK = dict(num_users=100, local_ep=10, local_bs=50, lr=0.1, rho=0.1, seed=2022, momentum=0.5,
+                    synthetic_train=6000, synthetic_test=200)
+DEC_NOTEBOOK_FRAC = 0.1
+DIST_NOTEBOOK = {
+    "WA_notebook_circle_stochastic": ("DecFedAvg", {"local_ep": 4, "local_bs": 128, "lr": 0.01}, None),
+    # the cell's default star / double_stochastic does not terminate in the shipped
+    # Sinkhorn loop (exact == 1 test); circle / double_stochastic does
+    "WA_notebook_circle_double": ("DecFedAvg", {"local_ep": 4, "local_bs": 128, "lr": 0.01,
+                                                "mode": "double_stochastic"}, None),
+}
 
 
 def main():
@@ -112,6 +129,13 @@ def main():
         r = run_dist(cls_name, over, eps)
         r.update(cls=cls_name, overrides=over, eps=eps)
         res["dist_variants"][key] = r
+    res["notebook"] = {"dec_args": DEC_NOTEBOOK, "frac": DEC_NOTEBOOK_FRAC, "stride": NB_STRIDE, "dist": {}}
+    for name in ("FedAvg_Server", "FedProx_Server", "FedAdmm_Server"):
+        res["notebook"][name] = run_dec(name, DEC_NOTEBOOK, DEC_NOTEBOOK_FRAC, 2, NB_STRIDE)
+    for key, (cls_name, over, eps) in DIST_NOTEBOOK.items():
+        r = run_dist(cls_name, over, eps, NB_STRIDE)
+        r.update(cls=cls_name, overrides=over, eps=eps)
+        res["notebook"]["dist"][key] = r
     with open(os.path.join(HERE, "trajectories.json"), "w") as f:
         json.dump(res, f)
     print("wrote trajectories.json")
