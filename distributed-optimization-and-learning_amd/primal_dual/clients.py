@@ -180,9 +180,14 @@ class FedAdmm_Client(Client):
         return loss, correct
 
     def update_duals(self, theta):
+        """alpha += rho (w - theta) (DEC/clients.py:141-144); the kernel also
+        leaves ||w - theta||^2 (fp64, fixed order) in self.resid_sq for the
+        server's per-round metrics (not part of the reference)."""
         b, i = self.bank, self.row
+        if getattr(self, "resid_sq", None) is None:
+            self.resid_sq = torch.zeros(1, dtype=torch.float64, device=b.device)
         ops.admm_dual(b.buffer("alpha")[i:i + 1], b.buffer("x")[i:i + 1], self.theta_vector(theta),
-                      self.args.rho, P=b.P)
+                      self.args.rho, resid_sq=self.resid_sq, P=b.P)
 
 
 _DEFAULT_UPDATE_MODEL = {None: FedAvg_Client.update_model, "prox": FedProx_Client.update_model,

@@ -35,6 +35,7 @@ class Server(object):
     def __init__(self, args):
         self.args = args
         self.history = []
+        self.metrics = []  # per-round primal / dual metrics (FedADMM), beside the reference's history
         self.global_round = 0
         setup_seed(args.seed)
         model = self.select_global_model(self.args.model, self.args.device)
@@ -99,6 +100,7 @@ class Server(object):
                 local_losses.append(loss)
             loss_avg = sum(local_losses) / len(local_losses)
             train_loss.append(loss_avg)
+            self._record_metrics(idxs_users)
             mean_acc_all, _ = self.avg_trainig_calculator()
             self.update_global_model(local_weights)
             test_acc_1, test_loss_1 = self.global_client.inference("test")
@@ -114,6 +116,21 @@ class Server(object):
         print("\n Total Run Time: {0:0.4f}".format(time.time() - start_time))
         print(f" \n Results after {rounds} global rounds of training:")
         print("|---- Test Accuracy: {:.2f}%".format(100 * test_acc[-1]))
+
+    def _record_metrics(self, idxs_users):
+        """Per-round primal / dual metrics of the sampled clients, kept
+        in self.metrics so the reference's `history` schema is unchanged:
+        primal_resid_sq = sum_k ||w_k - theta||^2 (pre-round theta, from the
+        dual kernel), dual_sq = sum_k ||alpha_k||^2 (FedADMM only)."""
+        cs = [self.clients[int(i)] for i in idxs_users]
+        if not cs or getattr(cs[0], "TERM", None) != "admm":
+            return
+        b = cs[0].bank
+        rows = torch.as_tensor([c.row for c in cs], device=b.device)
+        alpha = b.buffer("alpha")[rows, : b.P].double()
+        resid = torch.stack([c.resid_sq[0] for c in cs]).sum()
+        self.metrics.append({"round": self.global_round, "primal_resid_sq": float(resid),
+                             "dual_sq": float((alpha * alpha).sum())})
 
     def tarining(self):
         pass

@@ -367,3 +367,20 @@ def test_gossip_trajectory_at_notebook_shape(key, gpu):
     _check_history(sim.history, ref["history"], ("avg_test_acc",), args.synthetic_test)
     for c, r in zip(sim.clients, ref["agents"]):
         _check_summary(_flat(c.model), r, NB["stride"])
+
+
+def test_fedadmm_server_records_primal_dual_metrics(gpu):
+    """SURVEY §5 metrics: FedAdmm_Server.metrics holds, per round, the sampled
+    clients' sum ||w - theta||^2 (dual kernel's fp64 residual) and sum ||alpha||^2;
+    the reference's `history` keys are unchanged."""
+    m = load_project("primal_dual", ["servers", "utils"])
+    args = m["utils"].DotDict(dict(TRAJ["dec_args"], device="cuda"))
+    s = m["servers"].FedAdmm_Server(args)
+    s.run(TRAJ["frac"], 2)
+    assert set(s.history[0]) == {"round", "test_acc", "test_loss", "train_loss", "train_acc"}
+    assert [r["round"] for r in s.metrics] == [0, 1]
+    for r in s.metrics:
+        assert r["primal_resid_sq"] > 0 and r["dual_sq"] > 0
+    # round 0: alpha = rho (w - theta) from zero duals, so ||alpha||^2 = rho^2 ||w - theta||^2 (fp32 rounding)
+    r0 = s.metrics[0]
+    assert r0["dual_sq"] == pytest.approx(args.rho ** 2 * r0["primal_resid_sq"], rel=1e-5)

@@ -284,6 +284,38 @@ def test_full_size_ring_sampled_rows(gpu):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("N", [1024, 8192])
+def test_full_size_random_regular_sampled_rows(N, gpu):
+    """BASELINE config 3 at full size on the agent-major bank: a random
+    4-regular W over N agents x 2^20 (the XCD-pinned CSR kernel): sampled output
+    rows bit-exact against the oracle on their four input rows, and the
+    column-sum identity in fp64 on 64 columns."""
+    P = 1 << 20
+    plan = G.MixingPlan(G.random_regular_csr(N, 4, seed=2028), gpu)
+    g = torch.Generator(device=gpu).manual_seed(2)
+    X = torch.randn(N, P, device=gpu, generator=g)
+    Y = torch.empty_like(X)
+    plan.apply(X, Y)
+    torch.cuda.synchronize()
+    c = plan.csr
+    for i in [0, 1, N // 2, N - 1] + list(np.random.default_rng(1).integers(0, N, 8)):
+        i = int(i)
+        e0, e1 = int(c.rowptr[i]), int(c.rowptr[i + 1])
+        cols = c.col[e0:e1]
+        rows = X[torch.as_tensor(cols, dtype=torch.int64, device=gpu)].cpu().numpy()
+        want = oracle.mix_csr(rows, np.array([0, e1 - e0], np.int32), np.arange(e1 - e0, dtype=np.int32),
+                              c.val[e0:e1])[0]
+        assert bits_equal(Y[i].cpu().numpy(), want), i
+    cols = torch.arange(0, P, P // 64, device=gpu)
+    colw = np.zeros(N, np.float64)
+    np.add.at(colw, c.col, c.val.astype(np.float64))
+    lhs = Y[:, cols].double().sum(0)
+    rhs = (torch.from_numpy(colw).to(gpu)[:, None] * X[:, cols].double()).sum(0)
+    torch.testing.assert_close(lhs, rhs, rtol=1e-5, atol=1e-3)
+    del X, Y
+    torch.cuda.empty_cache()
+
+
 # --------------------------------------------------------------------------- dense (MFMA) mix
 def _gamma_bound(W, X):
     """Rigorous bound for an fp32 fma chain of length K: |Y - Y64| <= gamma_K * sum|W||X|,
