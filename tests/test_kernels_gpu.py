@@ -588,7 +588,7 @@ def test_prox_grad_term_vs_oracle(admm, extra, gpu):
 
 
 @pytest.mark.parametrize("steps", [1, 2, 3, 4, 5, 6, 7, 8])
-@pytest.mark.parametrize("n,P", [(3, 8), (17, 4100), (64, 1024 * 5)])
+@pytest.mark.parametrize("n,P", [(3, 8), (17, 4100), (64, 1024 * 5), (200, 1024), (1001, 2048)])
 def test_ring_steps_bit_identical_to_single_rounds(steps, n, P, gpu):
     rng = np.random.default_rng(steps * 100 + n)
     X = rng.standard_normal((n, P)).astype(np.float32)
