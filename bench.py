@@ -432,7 +432,7 @@ def main():
             "roofline": {
                 "bound": "hbm",
                 "kernel": ("ring_mix_kernel" if os.environ.get("DOL_RING_DMA", "1") == "0" else
-                           "ring_mix_dma_kernel<4, NoEpi, true>" if os.environ.get("DOL_RING_NTI", "1") != "0" else
+                           "ring_mix_dma_kernel<4, NoEpi, true, false>" if os.environ.get("DOL_RING_NTI", "1") != "0" else
                            "ring_mix_dma_kernel<4, NoEpi>"),
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBPS,

@@ -137,29 +137,82 @@ __device__ __forceinline__ f4 mix_quad(const Quad& Q, const float* __restrict__ 
   return y;
 }
 
+// Config-3 epilogue on the parameter-major bank (the DGD round of
+// dol_dgd_csr_f32, transposed): after the mix, `steps` local momentum-SGD
+// iterations on the separable loss, per coordinate (OBJ 0 least squares
+// g = x - t, 1 logistic g = -t / (1 + exp(t x)); MODE 0 plain SGD, 1 first
+// momentum step, 2 momentum), x = fma(-lr, d, x) — the arithmetic of DgdEpi /
+// oracle_dgd_local_f32.  The target (and momentum) p-rows of a stage come in
+// by the same LDS-DMA as X, behind the X image.
+struct PmDgd {
+  const float* T; int64_t ldt;
+  float* M; int64_t ldm;
+  float neg_lr, mom;
+  int steps;
+};
+
+template <int OBJ, int MODE>
+__device__ __forceinline__ float dgd_local(float x, float t, float& b, const PmDgd& e) {
+  for (int s = 0; s < e.steps; ++s) {
+    float g;
+    if constexpr (OBJ == 0) g = x - t;
+    else g = -t / (1.0f + expf(t * x));
+    float d = g;
+    if constexpr (MODE != 0) {
+      if (MODE == 1 && s == 0) b = g;
+      else b = b * e.mom + g;
+      d = b;
+    }
+    x = __builtin_fmaf(e.neg_lr, d, x);
+  }
+  return x;
+}
+
 // Mix one stage image (sr p-rows of xw floats at im0, p-rows p0 ..) and store
-// its rows of YT: spt buffer stores per thread, out-of-range ones dropped.
-template <int T, int QPT, int SAUX, bool COPY>
+// its rows of YT (and, OBJ >= 0, run the local steps first: target / momentum
+// images of nw floats per p-row follow the X image): spt (x2 with a momentum
+// store) buffer stores per thread, out-of-range ones dropped.
+template <int T, int QPT, int SAUX, bool COPY, int OBJ = -1, int MODE = 0>
 __device__ __forceinline__ void mix_stage(const Quad (&Q)[QPT], const float* __restrict__ im0, float* __restrict__ YT,
                                           int64_t ldy, int n_rows, int64_t P, int64_t p0, int xw, int sr, int spt,
                                           int q0, int g, int GR, const int32_t* __restrict__ rowptr,
-                                          const int32_t* __restrict__ col, const float* __restrict__ val) {
+                                          const int32_t* __restrict__ col, const float* __restrict__ val,
+                                          const PmDgd& e, int nw) {
   const int nq = (n_rows + 3) / 4;
   const int xq = xw / 4;
   const int64_t rows_here = std::min<int64_t>(sr, P - p0);
   const rsrc_t ry = make_rsrc(YT + p0 * ldy, static_cast<uint32_t>(rows_here * ldy * 4));
+  rsrc_t rm = ry;
+  if constexpr (OBJ >= 0 && MODE != 0) rm = make_rsrc(e.M + p0 * e.ldm, static_cast<uint32_t>(rows_here * e.ldm * 4));
+  const float* tim0 = im0 + sr * xw;      // target images
+  const float* mim0 = tim0 + sr * nw;     // momentum images (MODE 2)
   for (int u = 0; u < spt / QPT; ++u) {
     const int pr = g + u * GR;
     const bool prow_ok = pr < rows_here;
-    const float* im = im0 + (pr < sr ? pr : 0) * xw;
+    const int prc = pr < sr ? pr : 0;
+    const float* im = im0 + prc * xw;
 #pragma unroll
     for (int j = 0; j < QPT; ++j) {
       const int q = q0 + j * T;
-      const f4 y = COPY ? *reinterpret_cast<const f4*>(im + 4 * (q % xq)) : mix_quad(Q[j], im, q, rowptr, col, val);
+      f4 y = COPY ? *reinterpret_cast<const f4*>(im + 4 * (q % xq)) : mix_quad(Q[j], im, q, rowptr, col, val);
+      f4 bv = f4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (OBJ >= 0) {
+        const int qc = q < nq ? q : 0;
+        const f4 tv = *reinterpret_cast<const f4*>(tim0 + prc * nw + 4 * qc);
+        if constexpr (MODE == 2) bv = *reinterpret_cast<const f4*>(mim0 + prc * nw + 4 * qc);
+        float b0 = bv.x, b1 = bv.y, b2 = bv.z, b3 = bv.w;
+        y = f4{dgd_local<OBJ, MODE>(y.x, tv.x, b0, e), dgd_local<OBJ, MODE>(y.y, tv.y, b1, e),
+               dgd_local<OBJ, MODE>(y.z, tv.z, b2, e), dgd_local<OBJ, MODE>(y.w, tv.w, b3, e)};
+        bv = f4{b0, b1, b2, b3};
+      }
       const uint32_t off = static_cast<uint32_t>((pr * ldy + 4 * q) * 4);
+      const uint32_t offm = static_cast<uint32_t>((pr * (OBJ >= 0 && MODE != 0 ? e.ldm : 0) + 4 * q) * 4);
+      constexpr bool kMom = OBJ >= 0 && MODE != 0;
       if (4 * q + 3 < n_rows || q >= nq) {  // whole quad, or none (dropped)
         const bool ok = prow_ok && q < nq;
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, y), ry, ok ? off : kOOB, 0, SAUX);
+        if constexpr (kMom)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, bv), rm, ok ? offm : kOOB, 0, SAUX);
       } else {  // the ragged last quad (elements named one by one: hipcc 7.2 stored
                 // element 0 four times from a loop over y[a] here)
         const float ye[4] = {y.x, y.y, y.z, y.w};
@@ -169,6 +222,14 @@ __device__ __forceinline__ void mix_stage(const Quad (&Q)[QPT], const float* __r
                                               SAUX);
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ye[2]), ry, prow_ok && left > 2 ? off + 8 : kOOB, 0,
                                               SAUX);
+        if constexpr (kMom) {
+          const float be[4] = {bv.x, bv.y, bv.z, bv.w};
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(be[0]), rm, prow_ok ? offm : kOOB, 0, SAUX);
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(be[1]), rm, prow_ok && left > 1 ? offm + 4 : kOOB, 0,
+                                                SAUX);
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(be[2]), rm, prow_ok && left > 2 ? offm + 8 : kOOB, 0,
+                                                SAUX);
+        }
       }
     }
   }
@@ -178,13 +239,15 @@ __device__ __forceinline__ void mix_stage(const Quad (&Q)[QPT], const float* __r
 // quads per thread.  LAUX / SAUX: cache-policy bits of the LDS-DMA loads / the
 // stores (0 default, 2 nontemporal); COPY: y = x of the same agent (a copy in
 // the same geometry: the structure's own ceiling, measurement only).
-template <int T, int SF, int NBUF, int QPT, int LAUX, int SAUX, bool COPY = false>
+// OBJ >= 0: the config-3 epilogue (PmDgd), its target (+ momentum) p-rows
+// staged behind X's in every stage (nw floats each).
+template <int T, int SF, int NBUF, int QPT, int LAUX, int SAUX, bool COPY = false, int OBJ = -1, int MODE = 0>
 __global__ __launch_bounds__(T) void csr_pm_kernel(const float* __restrict__ XT, int64_t ldx, int x_rows,
                                                    float* __restrict__ YT, int64_t ldy, int n_rows, int64_t P,
                                                    int xw, int sr, int qp_log2, int spt, int64_t n_stages, int nseg,
                                                    const int32_t* __restrict__ rowptr,
                                                    const int32_t* __restrict__ col,
-                                                   const float* __restrict__ val) {
+                                                   const float* __restrict__ val, PmDgd e, int nw) {
   constexpr int kDma = SF / 4 / T;  // LDS-DMA instructions per thread per stage
   static_assert(kDma * 4 * T == SF, "a stage is a whole number of DMA rounds");
   extern __shared__ __attribute__((aligned(16))) float img[];  // NBUF x SF
@@ -215,18 +278,28 @@ __global__ __launch_bounds__(T) void csr_pm_kernel(const float* __restrict__ XT,
   auto stage_of = [&](int64_t k) { return seg * seg_len + wl + k * W; };
   const int xq = xw / 4;             // 16-B pieces per p-row image
   const int xr4 = (x_rows + 3) / 4;  // pieces holding data
+  const int nq4 = nw / 4, nr4 = (n_rows + 3) / 4;
+  const int nX = sr * xq, nTM = sr * nq4;  // pieces of the X images, of one epilogue operand's images
   auto issue = [&](int64_t k) {      // stage k of this workgroup -> buffer k % NBUF
     const int64_t p0 = stage_of(k) * sr;
     float* dst = img + (k % NBUF) * SF;
 #pragma unroll
     for (int d = 0; d < kDma; ++d) {
       const int pc = d * T + tid;
-      const int pr = pc / xq, j4 = pc - pr * xq;
-      const bool ok = pr < sr && p0 + pr < P && j4 < xr4;
-      const float* src = ok ? XT + (p0 + pr) * ldx + 4 * j4 : XT;  // dead pieces re-read XT[0..3]
+      const float* src = XT;  // dead pieces re-read XT[0..3]
+      if (pc < nX) {
+        const int pr = pc / xq, j4 = pc - pr * xq;
+        if (p0 + pr < P && j4 < xr4) src = XT + (p0 + pr) * ldx + 4 * j4;
+      } else if (OBJ >= 0) {
+        const int pt = pc - nX, op = pt / nTM, r = pt - op * nTM;  // op 0: target, 1: momentum
+        const int pr = r / nq4, j4 = r - pr * nq4;
+        if ((op == 0 || (MODE == 2 && op == 1)) && p0 + pr < P && j4 < nr4)
+          src = op == 0 ? e.T + (p0 + pr) * e.ldt + 4 * j4 : e.M + (p0 + pr) * e.ldm + 4 * j4;
+      }
       __builtin_amdgcn_global_load_lds(DOL_GPTR(src), DOL_LPTR(dst + (d * T + wave * 64) * 4), 16, 0, LAUX);
     }
   };
+  constexpr int kStores = (OBJ >= 0 && MODE != 0) ? 2 : 1;  // buffer stores per (p-row, quad)
 #pragma unroll
   for (int k = 0; k < NBUF - 1; ++k)
     if (k < nk) issue(k);
@@ -234,12 +307,13 @@ __global__ __launch_bounds__(T) void csr_pm_kernel(const float* __restrict__ XT,
     // retire stage k: younger ops are the stages issued after it and (k >= 1)
     // the previous stage's spt stores
     const int64_t ahead = std::min<int64_t>(nk - 1, k + NBUF - 2) - k;
-    wait_vmcnt(static_cast<int>((k >= 1 ? spt : 0) + kDma * ahead));
+    wait_vmcnt(static_cast<int>((k >= 1 ? kStores * spt : 0) + kDma * ahead));
     __builtin_amdgcn_s_barrier();  // every wave's share landed; buffer (k-1) % NBUF is free
     if (k + NBUF - 1 < nk) issue(k + NBUF - 1);
     const int64_t p0 = stage_of(k) * sr;
     const float* im0 = img + (k % NBUF) * SF;
-    mix_stage<T, QPT, SAUX, COPY>(Q, im0, YT, ldy, n_rows, P, p0, xw, sr, spt, q0, g, GR, rowptr, col, val);
+    mix_stage<T, QPT, SAUX, COPY, OBJ, MODE>(Q, im0, YT, ldy, n_rows, P, p0, xw, sr, spt, q0, g, GR, rowptr, col, val,
+                                            e, nw);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this stage's LDS reads are done before the next barrier
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -290,10 +364,14 @@ int n_cus() {
 
 extern "C" {
 
-int dol_mix_csr_pm_f32(const float* XT, int64_t ldx, int32_t x_rows, float* YT, int64_t ldy, int32_t n_rows,
-                       int64_t P, const int32_t* rowptr, const int32_t* col, const float* val, hipStream_t s) {
-  DOL_DIMS_OK("dol_mix_csr_pm_f32", ldx, ldy, P);
-  const char* nm = "dol_mix_csr_pm_f32";
+}  // extern "C"
+
+namespace {
+
+// obj < 0: the plain mix; else the config-3 round (epilogue e, momentum mode)
+int mix_csr_pm_impl(const char* nm, const float* XT, int64_t ldx, int32_t x_rows, float* YT, int64_t ldy,
+                    int32_t n_rows, int64_t P, const int32_t* rowptr, const int32_t* col, const float* val, int obj,
+                    int mode, const PmDgd& e, hipStream_t s) {
   if (n_rows < 0 || x_rows < 0 || P < 0) return fail(DOL_EINVAL, "%s: negative size", nm);
   if (n_rows == 0 || P == 0) { dol::g_err[0] = '\0'; return DOL_OK; }
   if (!XT || !YT || !rowptr || (x_rows > 0 && (!col || !val))) return fail(DOL_EINVAL, "%s: null pointer", nm);
@@ -307,16 +385,32 @@ int dol_mix_csr_pm_f32(const float* XT, int64_t ldx, int32_t x_rows, float* YT, 
   if (XT == YT) return fail(DOL_EINVAL, "%s: XT and YT alias (Jacobi mix needs two buffers)", nm);
   const int xw = (x_rows + 255) / 256 * 256;
   const int nq = (n_rows + 3) / 4;
+  const int nw = 4 * nq;                                  // epilogue image width (floats)
+  const int ne = obj < 0 ? 0 : (mode == 2 ? 2 : 1);       // epilogue operands staged per p-row
+  if (obj >= 0) {
+    if (!e.T || (mode != 0 && !e.M)) return fail(DOL_EINVAL, "%s: null target / momentum", nm);
+    if (e.ldt % 4 || e.ldt < nw || (mode != 0 && (e.ldm % 4 || e.ldm < nw)))
+      return fail(DOL_EINVAL, "%s: ldt / ldm must be multiples of 4 covering the rounded-up agent count", nm);
+    if ((reinterpret_cast<uintptr_t>(e.T) | (mode ? reinterpret_cast<uintptr_t>(e.M) : 0)) & 15u)
+      return fail(DOL_EINVAL, "%s: target / momentum must be 16-B aligned", nm);
+    if (nq > kT1 || xw > 4096) return fail(DOL_EINVAL, "%s: the fused round takes at most 4096 agents", nm);
+  }
   // geometry: 1024-thread workgroups, one per CU.  Up to 4096 agents (one quad
   // per thread): 64 KiB stages, 2 buffers; beyond (two quads per thread, a
   // p-row up to 32 KiB): 32 KiB stages, 4 buffers.  Measured at 1024 x 2^20
-  // (one box, tools/gpu_pm_cfg.sh): 64 KiB x 2 1.511 ms, 32 KiB x 4 1.533,
-  // 48 KiB x 3 1.541; 256- / 512-thread workgroups (8 / 16 KiB stages, 2-4 per
-  // CU) 1.82 / 1.64; one stage per short-lived workgroup 4.4; a per-wave ring
-  // (no workgroup barrier, 4 KiB p-rows, 176 VGPRs) 1.64.
+  // (one box): 64 KiB x 2 1.511 ms, 32 KiB x 4 1.533, 48 KiB x 3 1.541;
+  // 256- / 512-thread workgroups (8 / 16 KiB stages, 2-4 per CU) 1.82 / 1.64;
+  // one stage per short-lived workgroup 4.4; a per-wave ring (no workgroup
+  // barrier, 4 KiB p-rows, 176 VGPRs) 1.64.
   const bool big = nq > kT1 || xw > 4096;
-  const int SF = big ? 8192 : 16384, NB = big ? 4 : 2;
-  int sr = SF / xw;
+  // fused round: 64 KiB x 2 stages, or 80 KiB x 2 with the momentum read (1024
+  // x 2^20 rr4, one box, twice: least squares + momentum 3.45 ms vs 3.56 with
+  // 64 KiB x 2 and 3.49 with 48 KiB x 3; logistic, no momentum, 2.25 vs 2.43 /
+  // 2.55).  DOL_PM_DGD_GEOM (0 / 1 / 2) overrides, for measurement.
+  const int dgeo = obj >= 0 ? env_int("DOL_PM_DGD_GEOM", ne == 2 ? 2 : 0) : 0;
+  const int SF = big ? 8192 : (dgeo == 1 ? 12288 : dgeo == 2 ? 20480 : 16384);
+  const int NB = big ? 4 : (dgeo == 1 ? 3 : 2);
+  int sr = SF / (xw + ne * nw);
   int qp_log2 = 0, spt;
   if (!big) {
     while ((1 << qp_log2) < nq) ++qp_log2;
@@ -324,17 +418,18 @@ int dol_mix_csr_pm_f32(const float* XT, int64_t ldx, int32_t x_rows, float* YT, 
     if (sr >= gr) sr = std::min(sr / gr * gr, 4 * gr);
     spt = (sr + gr - 1) / gr;
   } else {
-
     sr = 1;
     spt = 2;
   }
-  if (int64_t(sr) * ldy * 4 >= (int64_t(1) << 31)) return fail(DOL_EINVAL, "%s: ldy too large", nm);
+  if (sr < 1) return fail(DOL_EINVAL, "%s: a p-row and its epilogue operands exceed a stage", nm);
+  if (int64_t(sr) * std::max(ldy, std::max(e.ldt, e.ldm)) * 4 >= (int64_t(1) << 31))
+    return fail(DOL_EINVAL, "%s: leading dimension too large", nm);
   const int64_t n_stages = (P + sr - 1) / sr;
   const int ncu = n_cus();
   if (ncu <= 0) return fail(DOL_EINVAL, "%s: no device", nm);
   // measurement knobs: DOL_PM_VARIANT 1 = default-policy DMA loads, 4 = copy in
   // this geometry (the structure's ceiling); DOL_PM_NSEG = stage-order segments
-  const int var = env_int("DOL_PM_VARIANT", 0);
+  const int var = obj < 0 ? env_int("DOL_PM_VARIANT", 0) : 0;
   auto go = [&](auto kern) {
     const int lds = NB * SF * 4;
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
@@ -342,18 +437,58 @@ int dol_mix_csr_pm_f32(const float* XT, int64_t ldx, int32_t x_rows, float* YT, 
     int nseg = env_int("DOL_PM_NSEG", 8);
     if (nseg < 1 || grid % nseg) nseg = 1;
     hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(grid)), dim3(kT1), lds, s, XT, ldx, x_rows, YT, ldy, n_rows, P,
-                       xw, sr, qp_log2, spt, n_stages, nseg, rowptr, col, val);
+                       xw, sr, qp_log2, spt, n_stages, nseg, rowptr, col, val, e, nw);
   };
+  using std::integral_constant;
+  if (obj >= 0) {  // small geometry only
+    auto ge = [&](auto oc, auto mc) {
+      constexpr int Oc = decltype(oc)::value, Mc = decltype(mc)::value;
+      if (dgeo == 1) go(csr_pm_kernel<kT1, 12288, 3, 1, 2, 2, false, Oc, Mc>);
+      else if (dgeo == 2) go(csr_pm_kernel<kT1, 20480, 2, 1, 2, 2, false, Oc, Mc>);
+      else go(csr_pm_kernel<kT1, 16384, 2, 1, 2, 2, false, Oc, Mc>);
+    };
+    using O0 = integral_constant<int, 0>;
+    using O1 = integral_constant<int, 1>;
+    using M0 = integral_constant<int, 0>;
+    using M1 = integral_constant<int, 1>;
+    using M2 = integral_constant<int, 2>;
+    if (obj == 0) { if (mode == 0) ge(O0{}, M0{}); else if (mode == 1) ge(O0{}, M1{}); else ge(O0{}, M2{}); }
+    else { if (mode == 0) ge(O1{}, M0{}); else if (mode == 1) ge(O1{}, M1{}); else ge(O1{}, M2{}); }
+    return check_launch(nm);
+  }
   auto pick = [&](auto sfc, auto nbc, auto qc) {
     constexpr int SFc = decltype(sfc)::value, NBc = decltype(nbc)::value, Qc = decltype(qc)::value;
     if (var == 1) go(csr_pm_kernel<kT1, SFc, NBc, Qc, 0, 2>);
     else if (var == 4) go(csr_pm_kernel<kT1, SFc, NBc, Qc, 2, 2, true>);
     else go(csr_pm_kernel<kT1, SFc, NBc, Qc, 2, 2>);
   };
-  using std::integral_constant;
   if (big) pick(integral_constant<int, 8192>{}, integral_constant<int, 4>{}, integral_constant<int, 2>{});
   else pick(integral_constant<int, 16384>{}, integral_constant<int, 2>{}, integral_constant<int, 1>{});
   return check_launch(nm);
+}
+
+}  // namespace
+
+extern "C" {
+
+int dol_mix_csr_pm_f32(const float* XT, int64_t ldx, int32_t x_rows, float* YT, int64_t ldy, int32_t n_rows,
+                       int64_t P, const int32_t* rowptr, const int32_t* col, const float* val, hipStream_t s) {
+  DOL_DIMS_OK("dol_mix_csr_pm_f32", ldx, ldy, P);
+  return mix_csr_pm_impl("dol_mix_csr_pm_f32", XT, ldx, x_rows, YT, ldy, n_rows, P, rowptr, col, val, -1, 0, PmDgd{},
+                         s);
+}
+
+int dol_dgd_csr_pm_f32(const float* XT, int64_t ldx, int32_t x_rows, float* YT, int64_t ldy, int32_t n_rows,
+                       int64_t P, const int32_t* rowptr, const int32_t* col, const float* val, const float* TT,
+                       int64_t ldt, float* MT, int64_t ldm, int32_t objective, int32_t local_steps, float lr,
+                       float momentum, int first_step, hipStream_t s) {
+  DOL_DIMS_OK("dol_dgd_csr_pm_f32", ldx, ldy, P, ldt, ldm);
+  const char* nm = "dol_dgd_csr_pm_f32";
+  if (objective != 0 && objective != 1) return fail(DOL_EINVAL, "%s: objective must be 0 or 1", nm);
+  if (local_steps < 1) return fail(DOL_EINVAL, "%s: local_steps must be >= 1", nm);
+  const int mode = momentum == 0.0f ? 0 : (first_step ? 1 : 2);
+  const PmDgd e{TT, ldt, mode ? MT : nullptr, mode ? ldm : 0, -lr, momentum, local_steps};
+  return mix_csr_pm_impl(nm, XT, ldx, x_rows, YT, ldy, n_rows, P, rowptr, col, val, objective, mode, e, s);
 }
 
 int dol_transpose_f32(const float* A, int64_t lda, float* B, int64_t ldb, int64_t rows, int64_t cols, hipStream_t s) {

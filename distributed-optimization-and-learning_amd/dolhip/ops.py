@@ -18,10 +18,11 @@ __all__ = [
     "mix_ring_steps", "prox_admm_sgd", "admm_dual", "ordered_mean",
     "ordered_sum", "stream_copy", "dual_workspace_bytes", "prox_grad", "admm_step_dual", "mlp_step",
     "dgd_ring", "dgd_csr", "OBJECTIVES", "admm_ls_round", "admm_ls_round_workspace_bytes", "mix_csr_pm",
-    "transpose", "PM_MAX_AGENTS", "stream_copy_rows",
+    "transpose", "PM_MAX_AGENTS", "stream_copy_rows", "dgd_csr_pm", "PM_DGD_MAX_AGENTS",
 ]
 
 PM_MAX_AGENTS = 8192  # dol_mix_csr_pm_f32: one p-row image (<= 32 KiB) per LDS stage
+PM_DGD_MAX_AGENTS = 4096  # dol_dgd_csr_pm_f32: X, target and momentum p-rows share a 64 KiB stage
 
 
 def _stream(t: torch.Tensor) -> int:
@@ -218,6 +219,49 @@ def dgd_csr(X: torch.Tensor, Y: torch.Tensor, rowptr: torch.Tensor, col: torch.T
                  target.data_ptr(), ldt, _ptr(mom) if ldm else None, ldm, OBJECTIVES[objective], int(steps),
                  float(lr), float(momentum), int(bool(first_step)), _stream(X))
     return Y
+
+
+def dgd_csr_pm(XT: torch.Tensor, YT: torch.Tensor, rowptr: torch.Tensor, col: torch.Tensor, val: torch.Tensor,
+               TT: torch.Tensor, MT: Optional[torch.Tensor] = None, objective: str = "least_squares",
+               steps: int = 1, lr: float = 0.01, momentum: float = 0.0, first_step: bool = False,
+               x_agents: Optional[int] = None, P: Optional[int] = None) -> torch.Tensor:
+    """dgd_csr on the parameter-major bank: XT/YT as mix_csr_pm, TT [P, >= n]
+    the targets and MT [P, >= n] the momentum (transposed like XT); the same
+    mix and local steps, bit-identical to dgd_csr on the transposed matrices.
+    At most PM_DGD_MAX_AGENTS agents."""
+    P = XT.shape[0] if P is None else P
+    n = rowptr.shape[0] - 1
+    x_agents = n if x_agents is None else int(x_agents)
+    ldx = _check_rows("XT", XT)
+    ldy = _check_rows("YT", YT)
+    if XT.shape[0] < P or YT.shape[0] < P:
+        raise ValueError(f"XT/YT need >= {P} parameter rows")
+    if XT.shape[1] < x_agents or YT.shape[1] < n:
+        raise ValueError(f"XT needs >= {x_agents} agent columns, YT >= {n}")
+    for nm, t, dt in (("rowptr", rowptr, torch.int32), ("col", col, torch.int32), ("val", val, torch.float32)):
+        if t.device != XT.device or t.dtype != dt or not t.is_contiguous():
+            raise ValueError(f"{nm}: expected contiguous {dt} on {XT.device}")
+    if XT.data_ptr() == YT.data_ptr():
+        raise ValueError("XT and YT alias: the Jacobi mix needs two buffers")
+    if objective not in OBJECTIVES:
+        raise ValueError(f"objective must be one of {sorted(OBJECTIVES)}")
+    if int(steps) < 1:
+        raise ValueError("local steps must be >= 1")
+    ldt = _check_rows("TT", TT)
+    if TT.shape[0] < P or TT.shape[1] < n or TT.device != XT.device:
+        raise ValueError(f"TT: expected [>= {P}, >= {n}] on {XT.device}")
+    ldm = 0
+    if momentum != 0.0:
+        if MT is None:
+            raise ValueError("momentum != 0 needs MT")
+        ldm = _check_rows("MT", MT)
+        if MT.shape[0] < P or MT.shape[1] < n or MT.device != XT.device:
+            raise ValueError(f"MT: expected [>= {P}, >= {n}] on {XT.device}")
+    _native.call("dol_dgd_csr_pm_f32", XT.data_ptr(), ldx, x_agents, YT.data_ptr(), ldy, n, P, rowptr.data_ptr(),
+                 col.data_ptr() if col.numel() else None, val.data_ptr() if val.numel() else None, TT.data_ptr(),
+                 ldt, _ptr(MT) if ldm else None, ldm, OBJECTIVES[objective], int(steps), float(lr), float(momentum),
+                 int(bool(first_step)), _stream(XT))
+    return YT
 
 
 def mix_dense(W: torch.Tensor, X: torch.Tensor, Y: torch.Tensor, P: Optional[int] = None) -> torch.Tensor:

@@ -176,6 +176,18 @@ int dol_dgd_csr_f32(const float* X, int64_t ldx, int32_t x_rows, float* Y, int64
                     const int32_t* rowptr, const int32_t* col, const float* val, const float* target, int64_t ldt,
                     float* mom, int64_t ldm, int32_t objective, int32_t local_steps, float lr, float momentum,
                     int first_step, hipStream_t s);
+/*
+ * dol_dgd_csr_f32 on the parameter-major bank (XT, YT as dol_mix_csr_pm_f32;
+ * TT [P][ldt] the targets and MT [P][ldm] the momentum, transposed the same
+ * way): the same mix, the same local steps, bit-identical results, one pass.
+ * Target and momentum p-rows ride the mix's LDS stages.  Limits: x_rows,
+ * n_rows <= 4096; ldt, ldm multiples of 4 >= round_up(n_rows, 4); TT, MT 16-B
+ * aligned; MT NULL iff momentum == 0 (then ldm is ignored).
+ */
+int dol_dgd_csr_pm_f32(const float* XT, int64_t ldx, int32_t x_rows, float* YT, int64_t ldy, int32_t n_rows,
+                       int64_t P, const int32_t* rowptr, const int32_t* col, const float* val, const float* TT,
+                       int64_t ldt, float* MT, int64_t ldm, int32_t objective, int32_t local_steps, float lr,
+                       float momentum, int first_step, hipStream_t s);
 
 /*
  * Fused local step of n_agents agents (rows of w/buf/g), replacing:

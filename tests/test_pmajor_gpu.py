@@ -158,3 +158,105 @@ def test_pm_mix_argument_errors(gpu):
         ops.mix_csr_pm(torch.zeros(10, 18, device=gpu)[:, :17], torch.zeros(10, 16, device=gpu), rp, col, val)
     with pytest.raises(ValueError, match="alias"):
         ops.mix_csr_pm(XT, XT, rp, col, val)
+
+
+# --- config 3's fused round on the parameter-major bank (dol_dgd_csr_pm_f32) ---
+
+def _dgd_pm(X, T, M, c, gpu, objective, steps, lr, momentum, first, extra=0):
+    rp, col, val = csr_dev(c, gpu)
+    n = len(c.rowptr) - 1
+    XT, TT = pm(X, gpu, extra), pm(T, gpu, extra)
+    MT = pm(M, gpu, extra) if momentum else None
+    YT = torch.full((X.shape[1], (n + 3) // 4 * 4 + extra), 7.0, device=gpu)
+    ops.dgd_csr_pm(XT, YT, rp, col, val, TT, MT, objective=objective, steps=steps, lr=lr, momentum=momentum,
+                   first_step=first, x_agents=X.shape[0])
+    torch.cuda.synchronize()
+    out = YT.cpu().numpy()
+    assert (out[:, n:] == 7.0).all(), "wrote past the last agent"
+    Mo = None
+    if momentum:
+        mo = MT.cpu().numpy()
+        assert np.isnan(mo[:, n:]).all(), "momentum written past the last agent"
+        Mo = np.ascontiguousarray(mo[:, :n].T)
+    return np.ascontiguousarray(out[:, :n].T), Mo
+
+
+MODES = [(0.0, False), (0.9, True), (0.9, False)]
+
+
+@pytest.mark.parametrize("momentum,first", MODES)
+@pytest.mark.parametrize("n", [5, 100, 1000, 1024, 1025, 2047, 4096])
+@pytest.mark.parametrize("P", [1, 7, 300])
+def test_pm_dgd_least_squares_vs_oracle(n, P, momentum, first, gpu):
+    """Least squares: bit-exact against oracle.mix_csr then oracle.dgd_local
+    (one rounding per operation on both sides), momentum written back."""
+    c = G.random_regular_csr(n, 4, seed=n + 11)
+    rng = np.random.default_rng(n + 13 * P)
+    X, T, M = (rng.standard_normal((n, P)).astype(np.float32) for _ in range(3))
+    got_y, got_m = _dgd_pm(X, T, M, c, gpu, "least_squares", 3, 0.05, momentum, first, extra=4 * (n % 2))
+    want_y, want_m = oracle.dgd_local(oracle.mix_csr(X, c.rowptr, c.col, c.val), T, M if momentum else None,
+                                      "least_squares", 3, 0.05, momentum, first)
+    assert bits_equal(got_y, want_y)
+    if momentum:
+        assert bits_equal(got_m, want_m)
+
+
+@pytest.mark.parametrize("momentum,first", MODES)
+@pytest.mark.parametrize("n,P", [(64, 100), (1000, 257), (4096, 33)])
+def test_pm_dgd_logistic_matches_agent_major_kernel(n, P, momentum, first, gpu):
+    """Logistic calls expf: bit-identical to the agent-major fused kernel
+    (dol_dgd_csr_f32, same device libm) and within test_dgd_gpu's stated
+    tolerance (rtol 2e-6, atol 1e-6) of the glibc oracle."""
+    c = G.random_regular_csr(n, 4, seed=n)
+    rng = np.random.default_rng(n + P)
+    X, T, M = (rng.standard_normal((n, P)).astype(np.float32) for _ in range(3))
+    got_y, got_m = _dgd_pm(X, T, M, c, gpu, "logistic", 2, 0.1, momentum, first)
+    rp, col, val = csr_dev(c, gpu)
+    Xd, Td = (torch.as_tensor(a, device=gpu) for a in (X, T))
+    Md = torch.as_tensor(M, device=gpu) if momentum else None
+    Yd = torch.empty_like(Xd)
+    ops.dgd_csr(Xd, Yd, rp, col, val, Td, Md, objective="logistic", steps=2, lr=0.1, momentum=momentum,
+                first_step=first)
+    assert bits_equal(got_y, Yd.cpu().numpy())
+    if momentum:
+        assert bits_equal(got_m, Md.cpu().numpy())
+    want_y, _ = oracle.dgd_local(oracle.mix_csr(X, c.rowptr, c.col, c.val), T, M if momentum else None,
+                                 "logistic", 2, 0.1, momentum, first)
+    np.testing.assert_allclose(got_y, want_y, rtol=2e-6, atol=1e-6)
+
+
+def test_pm_dgd_full_size_sampled_rows(gpu):
+    """BASELINE config 3's round at full size (1024 x 2^20, random 4-regular W,
+    least squares, 2 local steps, momentum 0.9 continuing): 48 sampled
+    parameter rows and the last one bit-exact vs the oracle, Y and momentum."""
+    n, P = 1024, 1 << 20
+    c = G.random_regular_csr(n, 4, seed=2028)
+    rp, col, val = csr_dev(c, gpu)
+    g = torch.Generator(device=gpu).manual_seed(5)
+    XT, TT, MT = (torch.empty(P, n, device=gpu).normal_(generator=g) for _ in range(3))
+    M0 = MT.clone()
+    YT = torch.empty_like(XT)
+    ops.dgd_csr_pm(XT, YT, rp, col, val, TT, MT, steps=2, lr=0.05, momentum=0.9)
+    torch.cuda.synchronize()
+    rows = torch.as_tensor(np.concatenate([np.random.default_rng(4).choice(P, 48, replace=False), [P - 1]]),
+                           device=gpu)
+    sel = [np.ascontiguousarray(a[rows].cpu().numpy().T) for a in (XT, TT, M0)]
+    want_y, want_m = oracle.dgd_local(oracle.mix_csr(sel[0], c.rowptr, c.col, c.val), sel[1], sel[2],
+                                      "least_squares", 2, 0.05, 0.9, False)
+    assert bits_equal(YT[rows].cpu().numpy().T, want_y)
+    assert bits_equal(MT[rows].cpu().numpy().T, want_m)
+
+
+def test_pm_dgd_argument_errors(gpu):
+    c = G.random_regular_csr(4100, 4, seed=1)
+    rp, col, val = csr_dev(c, gpu)
+    Z = torch.zeros(3, 4100, device=gpu)
+    with pytest.raises(ops.DolNativeError, match="at most 4096"):
+        ops.dgd_csr_pm(Z, Z.clone(), rp, col, val, Z.clone())
+    c = G.random_regular_csr(16, 4, seed=1)
+    rp, col, val = csr_dev(c, gpu)
+    XT = torch.zeros(10, 16, device=gpu)
+    with pytest.raises(ValueError, match="needs MT"):
+        ops.dgd_csr_pm(XT, XT.clone(), rp, col, val, XT.clone(), momentum=0.9)
+    with pytest.raises(ops.DolNativeError, match="ldt / ldm"):
+        ops.dgd_csr_pm(XT, XT.clone(), rp, col, val, torch.zeros(10, 18, device=gpu)[:, :17])

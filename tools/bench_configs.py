@@ -146,6 +146,51 @@ def dgd_round(N, P, topo, objective, momentum, steps, reps, dev):
     torch.cuda.empty_cache()
 
 
+def dgd_pm_round(N, P, topo, objective, momentum, steps, reps, dev):
+    """Config 3's fused round on the parameter-major bank (dol_dgd_csr_pm_f32):
+    XT, YT, TT (targets), MT (momentum) all [P, round_up(N, 4)]; algorithmic
+    bytes as dgd_round."""
+    from dolhip import ops
+    if topo == "ring":
+        torch.manual_seed(2028)
+        c = G.communication_csr("circle", "stochastic", N)[0]
+    else:
+        c = G.random_regular_csr(N, int(topo[2:]), seed=2028)
+    ld = (N + 3) // 4 * 4
+    g = torch.Generator(device=dev).manual_seed(7)
+    XT, TT = (torch.empty(P, ld, device=dev).normal_(generator=g) for _ in range(2))
+    YT = torch.empty_like(XT)
+    MT = torch.zeros_like(XT) if momentum else None
+    rp = torch.as_tensor(c.rowptr, dtype=torch.int32, device=dev)
+    col = torch.as_tensor(c.col, dtype=torch.int32, device=dev)
+    val = torch.as_tensor(c.val, dtype=torch.float32, device=dev)
+    state = {"first": True}
+
+    def one():
+        ops.dgd_csr_pm(XT, YT, rp, col, val, TT, MT, objective=objective, steps=steps, lr=0.01, momentum=momentum,
+                       first_step=state["first"])
+        state["first"] = False
+    for _ in range(2):
+        one()
+    torch.cuda.synchronize()
+    s_, e_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s_.record()
+    for _ in range(reps):
+        one()
+    e_.record()
+    torch.cuda.synchronize()
+    ms = s_.elapsed_time(e_) / reps
+    alg = N * P * 4 * (3 + (2 if momentum else 0))
+    print(json.dumps({"workload": "config3: fused DGD round (mix + %d local step%s), parameter-major bank"
+                                  % (steps, "s" * (steps > 1)),
+                      "topology": topo + "-pm", "kernel": "csr_pm + DGD epilogue", "objective": objective,
+                      "momentum": momentum, "agents": N, "params": P, "ms_per_round": ms, "rounds_per_s": 1e3 / ms,
+                      "algorithmic_bytes": alg, "GBps": alg / (ms / 1e3) / 1e9,
+                      "frac_of_8TBps": alg / (ms / 1e3) / 1e9 / 8000.0}), flush=True)
+    del XT, TT, YT, MT
+    torch.cuda.empty_cache()
+
+
 def pm_round(N, P, topo, reps, dev, X, Y):
     """One X <- W X round on the parameter-major bank (XT[p][j], p-row stride
     round_up(N, 4)), reusing X / Y's memory as XT / YT."""
@@ -189,6 +234,8 @@ def main():
     ap.add_argument("--mlp", type=int, nargs="*", default=[1024], help="agent counts for the config-5 MLP round")
     ap.add_argument("--dgd", type=int, nargs="*", default=[1024], help="agent counts for the config-3 DGD round")
     ap.add_argument("--dgd-topologies", nargs="+", default=["ring", "rr4"])
+    ap.add_argument("--dgd-pm", type=int, nargs="*", default=[1024],
+                    help="agent counts for the config-3 round on the parameter-major bank")
     a = ap.parse_args()
     dev = torch.device("cuda")
     P = a.params
@@ -198,6 +245,10 @@ def main():
         for topo in a.dgd_topologies:
             dgd_round(N, P, topo, "least_squares", 0.5, 1, a.reps, dev)
             dgd_round(N, P, topo, "logistic", 0.0, 1, a.reps, dev)
+    for N in a.dgd_pm:
+        for topo in a.dgd_topologies:
+            dgd_pm_round(N, P, topo, "least_squares", 0.5, 1, a.reps, dev)
+            dgd_pm_round(N, P, topo, "logistic", 0.0, 1, a.reps, dev)
     for N in a.agents:
         ld = row_stride(P)
         X = torch.empty(N, ld, device=dev).normal_()
