@@ -239,3 +239,73 @@ class SeparableADMM:
     def distance_to_fixed_point(self) -> float:
         """||theta - theta*|| / sqrt(P) (full participation)."""
         return float((self.theta[:self.P].double() - self.fixed_point()).norm() / self.P ** 0.5)
+
+
+class SeparableDGDPM:
+    """Config 3 on the parameter-major bank: the round of SeparableDGD (same
+    objectives, same round order, bit-identical values) with every state
+    matrix stored transposed, XT[p][i] = agent i's parameter p ([P, ld], ld =
+    round_up(N, 4)), so that any sparse W streams the bank once
+    (dol_dgd_csr_pm_f32).  Build it from a SeparableDGD
+    (`from_agent_major`, which transposes that problem's current state) or
+    fresh (random init drawn directly in this layout).  At most
+    ops.PM_DGD_MAX_AGENTS agents."""
+
+    def __init__(self, plan: MixingPlan, P: int, objective: str = "least_squares", lr: float = 0.01,
+                 momentum: float = 0.0, local_steps: int = 1, seed: int = 2028, _state=None):
+        from . import ops
+        if plan.n_rows > ops.PM_DGD_MAX_AGENTS:
+            raise ValueError(f"the parameter-major round takes at most {ops.PM_DGD_MAX_AGENTS} agents")
+        if plan.kind == "dense":
+            raise ValueError("the parameter-major round mixes a sparse (CSR) W")
+        self.plan, self.P, self.objective = plan, int(P), objective
+        self.lr, self.mu, self.local_steps = float(lr), float(momentum), int(local_steps)
+        self.N = plan.n_rows
+        self.ld = (self.N + 3) // 4 * 4
+        dev = plan.device
+        shape = (self.P, self.ld)
+        self.XT = torch.zeros(shape, dtype=torch.float32, device=dev)
+        self.YT = torch.zeros_like(self.XT)
+        self.TT = torch.zeros_like(self.XT)
+        self.MT = torch.zeros_like(self.XT) if self.mu != 0.0 else None
+        self.first, self.rounds = True, 0
+        if _state is None:
+            g = torch.Generator(device=dev).manual_seed(seed)
+            self.XT[:, :self.N].normal_(generator=g)
+            self.TT[:, :self.N].normal_(generator=g)
+            if objective == "logistic":
+                t = self.TT[:, :self.N]
+                t.copy_(torch.where(torch.rand(t.shape, generator=g, device=dev) < 0.5, -t, t))
+
+    @classmethod
+    def from_agent_major(cls, prob: "SeparableDGD") -> "SeparableDGDPM":
+        """Transpose prob's current state (x, targets, momentum, first-step flag)."""
+        from . import ops
+        self = cls(prob.plan, prob.P, prob.objective, prob.lr, prob.mu, prob.local_steps, _state=True)
+        ops.transpose(prob.params(), self.XT, prob.plan.n_rows, prob.P)
+        ops.transpose(prob.targets(), self.TT, prob.plan.n_rows, prob.P)
+        if self.MT is not None:
+            ops.transpose(prob.momentum_rows(), self.MT, prob.plan.n_rows, prob.P)
+        self.first, self.rounds = prob.first, prob.rounds
+        return self
+
+    def round(self) -> None:
+        """X <- W X, then the local steps (one kernel); swaps XT / YT."""
+        from . import ops
+        p = self.plan
+        ops.dgd_csr_pm(self.XT, self.YT, p.rowptr, p.col, p.val, self.TT, self.MT, objective=self.objective,
+                       steps=self.local_steps, lr=self.lr, momentum=self.mu, first_step=self.first, P=self.P)
+        self.XT, self.YT = self.YT, self.XT
+        self.first = False
+        self.rounds += 1
+
+    def params(self) -> torch.Tensor:
+        """Agent-major copy [N, P] of the current parameters (diagnostic)."""
+        return self.XT[:, :self.N].T.contiguous()
+
+    def momentum_rows(self) -> Optional[torch.Tensor]:
+        return None if self.MT is None else self.MT[:, :self.N].T.contiguous()
+
+    def consensus_error(self) -> float:
+        x = self.XT[:, :self.N]
+        return float((x - x.mean(1, keepdim=True)).norm() / max(1, self.N) ** 0.5)
