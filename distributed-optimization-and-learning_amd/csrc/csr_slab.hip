@@ -1,0 +1,447 @@
+// csr_slab.hip — high-degree sparse mix on the agent-major bank, gathered from LDS.
+//
+// Same operation, same reference code and the same bits as dol_mix_csr_f32
+// (DIST/simulators.py:91-97 Neighbors: j ascending, W_ij > 0 kept;
+// DIST/clients.py:61-69 consensus: acc = +0; acc = fl(acc + fl(x_j * a_ij))),
+// for graphs whose rows have tens to thousands of neighbours: the Erdos-Renyi
+// p = 0.1 W of BASELINE config 5 (about 100 neighbours per row at 1024 agents,
+// 820 at 8192), drawn anew every round.  The agent-major CSR kernel fetches
+// every neighbour row from L2 (deg L2 reads per output element); the dense
+// split3 GEMM runs six bf16 MFMAs per W entry, 90 % of which are zeros, and is
+// not bit-exact.  Here each X value is read from HBM once per row group and
+// from LDS once per (output row, neighbour):
+//
+//   * a workgroup (16 waves) owns one SLAB = 256 columns of P and a ROW GROUP
+//     of 16 * RW output rows, RW per wave, held in registers (f4 per row per
+//     lane: lane l owns columns 4l .. 4l+3 of the slab);
+//   * the slab's X columns stream through LDS in CHUNKS of 64 agents (64 x 1 KiB,
+//     LDS-DMA global_load_lds_dwordx4: each agent's 1 KiB piece is contiguous
+//     in HBM and lands contiguous in LDS), double-buffered;
+//   * the CSR is re-packed chunk-major (dol_csr_slab_pack): for row group g
+//     and chunk k, the entries of the group's rows whose columns fall in the
+//     chunk form one contiguous block, (LDS byte offset of the agent's piece,
+//     weight bits) pairs in (row, column) order; hdr[g][k][i] = the block's
+//     first entry of row i.  Each block rides the chunk's LDS-DMA into LDS
+//     beside the X chunk, so the gather loop reads its indices from LDS
+//     (in-order, ~120-cycle reads, prefetched a step ahead) instead of scalar
+//     loads from L2 (out-of-order returns force a full drain per use: measured
+//     2.1 ms vs 0.24 ms of staging at 1024 x 101,770);
+//   * four rows walk their chunk entries in lockstep, two per row per step:
+//     one conflict-free ds_read_b128 (1 KiB: the wave reads one agent's whole
+//     piece) + 4 separately rounded mul / add per neighbour.  Chunks are
+//     visited in ascending agent order, so each row's sum runs over its CSR
+//     entries in exactly the reference's order.
+//
+// Bounds: LDS bytes = nnz * 1 KiB per slab (256 B/clk/CU), VALU = 5 wave
+// instructions per (neighbour, slab) (address add, 2 packed mul, 2 packed
+// add).  The row groups of one slab sit on one XCD at the same time
+// (blockIdx % 8 = XCD), so the slab's chunks come from HBM once and from that
+// XCD's L2 for the others.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdlib.h>
+
+#include "../../include/dol_hip.h"
+#include "dol_common.h"
+
+namespace {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+constexpr int kCols = 256;                 // slab width (floats): one f4 per lane
+constexpr int kChunk = DOL_SLAB_CHUNK;     // agents per LDS chunk
+constexpr int kWaves = 16;
+constexpr int kThreads = 64 * kWaves;
+constexpr int kXBytes = kChunk * kCols * 4;  // 64 KiB of X per chunk
+constexpr int kIdxBytes = 16 * 1024;          // index block capacity per chunk (2048 entries)
+constexpr int kBuf = kXBytes + kIdxBytes;     // one stage
+constexpr int kLds = 2 * kBuf;                // double buffer: 160 KiB
+constexpr int kRW = 8;                        // rows per wave
+constexpr int kRows = kWaves * kRW;           // rows per row group
+constexpr int kEntPad = 160;                  // ent pad entries (the block DMA may read 1 KiB + 8 B past a block)
+constexpr int kPerWave = kChunk / kWaves;  // DMA pieces per wave per chunk
+static_assert(kChunk % kWaves == 0, "chunk must split evenly over the waves");
+
+#define DOL_GPTR(p) ((const __attribute__((address_space(1))) void*)(p))
+#define DOL_LPTR(p) ((__attribute__((address_space(3))) void*)(p))
+
+struct I2 {
+  int32_t x, y;  // (LDS byte offset of the neighbour's piece in its chunk, weight bits)
+};
+
+__device__ __forceinline__ f4 fmac(f4 acc, float w, f4 x) {  // separately rounded mul, then add
+  return acc + x * w;
+}
+
+// PROBE (diagnostics, DOL_SLAB_PROBE): 1 = staging only (no gathers), 2 = gathers
+// only (no LDS-DMA: sums of whatever LDS holds; results meaningless).
+template <int PROBE = 0>
+__global__ __launch_bounds__(kThreads) void csr_slab_kernel(
+    const float* __restrict__ X, int64_t ldx, int x_rows, float* __restrict__ Y, int64_t ldy, int n_rows, int64_t P,
+    const int32_t* __restrict__ ent, const int32_t* __restrict__ hdr, int nk, int n_rg, int64_t n_slabs) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const uint32_t b = blockIdx.x;
+  const uint32_t xcd = b & 7u, local = b >> 3;
+  const int rg = int(local % uint32_t(n_rg));
+  const int64_t slab = int64_t(local / uint32_t(n_rg)) * 8 + xcd;
+  if (slab >= n_slabs) return;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t p = slab * kCols + lane * 4;       // this lane's first column
+  const int64_t pl = p + 4 <= ldx ? p : ldx - 4;   // in-bounds DMA column (lanes past P: values unused)
+  const float* xsrc = X + pl;
+  const int32_t* H = hdr + int64_t(rg) * nk * (kRows + 1);  // this row group's blocks
+  const uint8_t* entb = reinterpret_cast<const uint8_t*>(ent);
+
+  auto issue = [&](int k) {
+    if constexpr (PROBE == 2) return;
+    uint8_t* dst = lds + (k & 1) * kBuf;
+#pragma unroll
+    for (int i = 0; i < kPerWave; ++i) {
+      const int al = wave * kPerWave + i;
+      const int a = min(k * kChunk + al, x_rows - 1);  // agents past x_rows: never referenced
+      __builtin_amdgcn_global_load_lds(DOL_GPTR(xsrc + int64_t(a) * ldx), DOL_LPTR(dst + al * 1024), 16, 0, 0);
+    }
+    // the chunk's index block (16-B aligned start, whole 1 KiB pieces; ent is padded)
+    const int64_t e0 = H[int64_t(k) * (kRows + 1)], e1 = H[int64_t(k) * (kRows + 1) + kRows];
+    const int64_t a0 = (e0 * 8) & ~int64_t(15);
+    const int64_t nbytes = e1 * 8 - a0;
+    if (nbytes <= kIdxBytes && wave * 1024 < nbytes)
+      __builtin_amdgcn_global_load_lds(DOL_GPTR(entb + a0 + wave * 1024 + lane * 16),
+                                       DOL_LPTR(dst + kXBytes + wave * 1024), 16, 0, 0);
+  };
+
+  const int row0 = wave * kRW;  // within the group
+  f4 acc[kRW];
+#pragma unroll
+  for (int r = 0; r < kRW; ++r) acc[r] = f4{0.f, 0.f, 0.f, 0.f};
+  const uint32_t lane16 = uint32_t(lane) * 16;
+
+  issue(0);
+  for (int k = 0; k < nk; ++k) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // my pieces of chunk k landed
+    __syncthreads();                                   // ... and every wave's; buffer (k+1)&1 is free
+    if (k + 1 < nk) issue(k + 1);
+    if constexpr (PROBE == 1) continue;
+    const uint32_t xbase = uint32_t((k & 1) * kBuf) + lane16;  // LDS byte address of my X piece
+    const int32_t* hk = H + int64_t(k) * (kRows + 1);
+    const int e0 = hk[0];
+    const int sh = e0 & 1;                    // the block starts 8 B into its first 16-B piece
+    const bool fits = int64_t(hk[kRows]) * 8 - ((int64_t(e0) * 8) & ~int64_t(15)) <= kIdxBytes;
+    int bnd[kRW + 1];
+#pragma unroll
+    for (int i = 0; i <= kRW; ++i) bnd[i] = hk[row0 + i];
+    if (!fits) {  // an over-full block (denser graphs): indices from global memory, same order
+#pragma unroll
+      for (int r = 0; r < kRW; ++r)
+        for (int e = bnd[r]; e < bnd[r + 1]; ++e)
+          acc[r] = fmac(acc[r], __int_as_float(ent[2 * int64_t(e) + 1]),
+                        *reinterpret_cast<const f4*>(lds + xbase + ent[2 * int64_t(e)]));
+      continue;
+    }
+    const uint8_t* ib = lds + (k & 1) * kBuf + kXBytes + 8 * (sh - e0);  // entry e at ib + 8 e
+    // Rows in groups of four: lane j of the wave holds the group's entry j
+    // (LDS byte offset, weight) in two VGPRs; each neighbour's pair reaches
+    // the scalar unit by v_readlane (no memory latency inside the row loops).
+#pragma unroll
+    for (int g = 0; g < kRW / 4; ++g) {
+      const int gs = bnd[4 * g], ge = bnd[4 * g + 4];
+      if (ge == gs) continue;
+      if (ge - gs > 64) {  // a group with more than 64 entries in this chunk: uniform LDS reads
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          f4 a = acc[4 * g + i];
+          for (int e = bnd[4 * g + i]; e < bnd[4 * g + i + 1]; ++e) {
+            const I2 q = *reinterpret_cast<const I2*>(ib + 8 * e);
+            a = fmac(a, __int_as_float(q.y), *reinterpret_cast<const f4*>(lds + xbase + q.x));
+          }
+          acc[4 * g + i] = a;
+        }
+        continue;
+      }
+      const I2 q = *reinterpret_cast<const I2*>(ib + 8 * min(gs + lane, ge - 1));
+      const int vo = q.x, vw = q.y;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int j1 = bnd[4 * g + i + 1] - gs;
+        int j = bnd[4 * g + i] - gs;
+        f4 a = acc[4 * g + i];
+        for (; j + 4 <= j1; j += 4) {
+          const uint32_t o0 = __builtin_amdgcn_readlane(vo, j), o1 = __builtin_amdgcn_readlane(vo, j + 1);
+          const uint32_t o2 = __builtin_amdgcn_readlane(vo, j + 2), o3 = __builtin_amdgcn_readlane(vo, j + 3);
+          const f4 x0 = *reinterpret_cast<const f4*>(lds + xbase + o0);
+          const f4 x1 = *reinterpret_cast<const f4*>(lds + xbase + o1);
+          const f4 x2 = *reinterpret_cast<const f4*>(lds + xbase + o2);
+          const f4 x3 = *reinterpret_cast<const f4*>(lds + xbase + o3);
+          a = fmac(a, __int_as_float(__builtin_amdgcn_readlane(vw, j)), x0);
+          a = fmac(a, __int_as_float(__builtin_amdgcn_readlane(vw, j + 1)), x1);
+          a = fmac(a, __int_as_float(__builtin_amdgcn_readlane(vw, j + 2)), x2);
+          a = fmac(a, __int_as_float(__builtin_amdgcn_readlane(vw, j + 3)), x3);
+        }
+        if (j + 2 <= j1) {
+          const uint32_t o0 = __builtin_amdgcn_readlane(vo, j), o1 = __builtin_amdgcn_readlane(vo, j + 1);
+          const f4 x0 = *reinterpret_cast<const f4*>(lds + xbase + o0);
+          const f4 x1 = *reinterpret_cast<const f4*>(lds + xbase + o1);
+          a = fmac(a, __int_as_float(__builtin_amdgcn_readlane(vw, j)), x0);
+          a = fmac(a, __int_as_float(__builtin_amdgcn_readlane(vw, j + 1)), x1);
+          j += 2;
+        }
+        if (j < j1)
+          a = fmac(a, __int_as_float(__builtin_amdgcn_readlane(vw, j)),
+                   *reinterpret_cast<const f4*>(lds + xbase + uint32_t(__builtin_amdgcn_readlane(vo, j))));
+        acc[4 * g + i] = a;
+      }
+    }
+  }
+  if (p >= P) return;
+  const int grow0 = rg * kRows + row0;
+#pragma unroll
+  for (int r = 0; r < kRW; ++r) {
+    if (grow0 + r < n_rows) {
+      float* y = Y + int64_t(grow0 + r) * ldy + p;
+      if (p + 4 <= P) {
+        __builtin_nontemporal_store(acc[r], reinterpret_cast<f4*>(y));
+      } else {
+        for (int c = 0; c < int(P - p); ++c) y[c] = acc[r][c];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Dense W -> CSR (+ chunk starts) on the device, for a W drawn every round.
+// Selection rule of Neighbors (DIST/simulators.py:91-97): W_ij > 0 (NaN and
+// <= 0 dropped), j ascending.
+// ---------------------------------------------------------------------------
+constexpr int kRowThreads = 256;
+
+__global__ __launch_bounds__(kRowThreads) void dense_count_kernel(const float* __restrict__ W, int64_t ldw, int n_cols,
+                                                                  int32_t* __restrict__ rowptr) {
+  __shared__ int part[kRowThreads / 64];
+  const float* row = W + int64_t(blockIdx.x) * ldw;
+  int c = 0;
+  for (int j = threadIdx.x; j < n_cols; j += kRowThreads) c += row[j] > 0.f;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int t = 0;
+    for (int w = 0; w < kRowThreads / 64; ++w) t += part[w];
+    rowptr[blockIdx.x + 1] = t;
+  }
+}
+
+// in-place inclusive scan of rowptr[1..n] (one workgroup), rowptr[0] = 0
+__global__ __launch_bounds__(1024) void rowptr_scan_kernel(int32_t* __restrict__ rowptr, int n) {
+  __shared__ int wsum[16];
+  __shared__ int carry;
+  if (threadIdx.x == 0) {
+    carry = 0;
+    rowptr[0] = 0;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int base = 0; base < n; base += 1024) {
+    const int i = base + int(threadIdx.x);
+    int v = i < n ? rowptr[i + 1] : 0;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {  // inclusive wave scan
+      const int t = __shfl_up(v, o);
+      if (lane >= o) v += t;
+    }
+    if (lane == 63) wsum[w] = v;
+    __syncthreads();
+    int off = carry;
+    for (int q = 0; q < w; ++q) off += wsum[q];
+    if (i < n) rowptr[i + 1] = v + off;
+    __syncthreads();
+    if (threadIdx.x == 1023) carry = v + off;
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(kRowThreads) void dense_fill_kernel(const float* __restrict__ W, int64_t ldw, int n_cols,
+                                                                 const int32_t* __restrict__ rowptr,
+                                                                 int32_t* __restrict__ col, float* __restrict__ val) {
+  __shared__ int wcnt[kRowThreads / 64];
+  const int r = blockIdx.x;
+  const float* row = W + int64_t(r) * ldw;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int run = rowptr[r];
+  for (int t0 = 0; t0 < n_cols; t0 += kRowThreads) {
+    const int j = t0 + int(threadIdx.x);
+    const float v = j < n_cols ? row[j] : 0.f;
+    const bool keep = v > 0.f;
+    const uint64_t m = __ballot(keep);
+    const int below = __popcll(m & ((uint64_t(1) << lane) - 1));
+    if (lane == 0) wcnt[w] = __popcll(m);
+    __syncthreads();
+    int off = run;
+    for (int q = 0; q < w; ++q) off += wcnt[q];
+    if (keep) {
+      col[off + below] = j;
+      val[off + below] = v;
+    }
+    for (int q = w; q < kRowThreads / 64; ++q) off += wcnt[q];
+    run = off;
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Chunk-major packing of a device CSR (dol_csr_slab_pack).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int lower_bound_col(const int32_t* __restrict__ col, int lo, int hi, int key) {
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (col[mid] < key) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// hdr[g][k][i] <- number of row (g R + i)'s entries in chunk k (0 for i == R and rows past n_rows)
+__global__ __launch_bounds__(256) void slab_count_kernel(const int32_t* __restrict__ rowptr,
+                                                         const int32_t* __restrict__ col, int n_rows, int nk,
+                                                         int64_t len, int32_t* __restrict__ hdr) {
+  const int64_t idx = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (idx >= len) return;
+  const int i = int(idx % (kRows + 1));
+  const int64_t gk = idx / (kRows + 1);
+  const int k = int(gk % nk), g = int(gk / nk);
+  const int r = g * kRows + i;
+  int c = 0;
+  if (i < kRows && r < n_rows) {
+    const int e0 = rowptr[r], e1 = rowptr[r + 1];
+    const int lo = lower_bound_col(col, e0, e1, k * kChunk);
+    c = lower_bound_col(col, lo, e1, (k + 1) * kChunk) - lo;
+  }
+  hdr[idx] = c;
+}
+
+// in-place exclusive scan of hdr[0..len) (one workgroup: a contiguous segment per thread)
+__global__ __launch_bounds__(1024) void slab_scan_kernel(int32_t* __restrict__ hdr, int64_t len) {
+  __shared__ int wsum[16];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int64_t seg = (len + 1023) / 1024;
+  const int64_t b0 = min(len, int64_t(t) * seg), b1 = min(len, b0 + seg);
+  int s = 0;
+  for (int64_t j = b0; j < b1; ++j) s += hdr[j];
+  int v = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = __shfl_up(v, o);
+    if (lane >= o) v += u;
+  }
+  if (lane == 63) wsum[w] = v;
+  __syncthreads();
+  int off = v - s;
+  for (int q = 0; q < w; ++q) off += wsum[q];
+  for (int64_t j = b0; j < b1; ++j) {
+    const int c = hdr[j];
+    hdr[j] = off;
+    off += c;
+  }
+}
+
+// one wave per row: entries to their chunk-major slots as (LDS byte offset, weight bits)
+__global__ __launch_bounds__(64) void slab_scatter_kernel(const int32_t* __restrict__ rowptr,
+                                                          const int32_t* __restrict__ col,
+                                                          const float* __restrict__ val, int nk,
+                                                          const int32_t* __restrict__ hdr, int32_t* __restrict__ ent) {
+  const int r = blockIdx.x, g = r / kRows, i = r % kRows;
+  const int e0 = rowptr[r], e1 = rowptr[r + 1];
+  for (int e = e0 + int(threadIdx.x); e < e1; e += 64) {
+    const int c = col[e], k = c / kChunk;
+    const int first = lower_bound_col(col, e0, e1, k * kChunk);
+    const int64_t dst = hdr[(int64_t(g) * nk + k) * (kRows + 1) + i] + (e - first);
+    ent[2 * dst] = (c % kChunk) * (kCols * 4);
+    ent[2 * dst + 1] = __float_as_int(val[e]);
+  }
+}
+
+inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+}  // namespace
+
+extern "C" int dol_csr_slab_nk(int32_t x_rows) { return x_rows <= 0 ? 0 : int((int64_t(x_rows) + kChunk - 1) / kChunk); }
+extern "C" int64_t dol_csr_slab_hdr_len(int32_t n_rows, int32_t x_rows) {
+  if (n_rows <= 0 || x_rows <= 0) return 0;
+  return cdiv(n_rows, kRows) * dol_csr_slab_nk(x_rows) * (kRows + 1);
+}
+extern "C" int64_t dol_csr_slab_ent_len(int64_t nnz_cap) {
+  if (nnz_cap < 0 || nnz_cap > dol::kMaxDim) return 0;
+  return 2 * (nnz_cap + kEntPad);
+}
+
+extern "C" int dol_mix_csr_slab_f32(const float* X, int64_t ldx, int32_t x_rows, float* Y, int64_t ldy,
+                                    int32_t n_rows, int64_t P, const int32_t* ent, const int32_t* hdr,
+                                    hipStream_t s) {
+  DOL_DIMS_OK("dol_mix_csr_slab_f32", ldx, ldy, P);
+  using dol::fail;
+  if (n_rows < 0 || x_rows < 0 || P < 0) return fail(DOL_EINVAL, "dol_mix_csr_slab_f32: negative size");
+  if (n_rows == 0 || P == 0) return DOL_OK;
+  if (x_rows == 0) return fail(DOL_EINVAL, "dol_mix_csr_slab_f32: x_rows == 0");
+  if (!X || !Y || !ent || !hdr) return fail(DOL_EINVAL, "dol_mix_csr_slab_f32: null pointer");
+  if (X == Y) return fail(DOL_EINVAL, "dol_mix_csr_slab_f32: X and Y alias");
+  const int64_t p4 = (P + 3) / 4 * 4;
+  if (ldx % 4 || ldy % 4 || ldx < p4 || ldy < P)
+    return fail(DOL_EINVAL, "dol_mix_csr_slab_f32: need ldx, ldy multiples of 4, ldx >= round_up(P, 4), ldy >= P");
+  if (reinterpret_cast<uintptr_t>(X) % 16 || reinterpret_cast<uintptr_t>(Y) % 16 ||
+      reinterpret_cast<uintptr_t>(ent) % 16)
+    return fail(DOL_EINVAL, "dol_mix_csr_slab_f32: X, Y and ent must be 16-B aligned");
+  const int nk = dol_csr_slab_nk(x_rows);
+  const int64_t n_rg = cdiv(n_rows, kRows);
+  const int64_t n_slabs = cdiv(P, kCols);
+  const int64_t grid = 8 * cdiv(n_slabs, 8) * n_rg;
+  if (grid >= (int64_t(1) << 32)) return fail(DOL_EINVAL, "dol_mix_csr_slab_f32: too many workgroups");
+  static const int probe = [] { const char* e = getenv("DOL_SLAB_PROBE"); return e ? atoi(e) : 0; }();
+  auto launch = [&](auto kern) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
+    hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(grid)), dim3(kThreads), kLds, s, X, ldx, x_rows, Y, ldy,
+                       n_rows, P, ent, hdr, nk, static_cast<int>(n_rg), n_slabs);
+  };
+  if (probe == 1) launch(csr_slab_kernel<1>);
+  else if (probe == 2) launch(csr_slab_kernel<2>);
+  else launch(csr_slab_kernel<0>);
+  return dol::check_launch("dol_mix_csr_slab_f32");
+}
+
+extern "C" int dol_csr_slab_pack(const int32_t* rowptr, const int32_t* col, const float* val, int32_t n_rows,
+                                 int32_t x_rows, int32_t* ent, int32_t* hdr, hipStream_t s) {
+  using dol::fail;
+  if (n_rows < 0 || x_rows < 0) return fail(DOL_EINVAL, "dol_csr_slab_pack: negative size");
+  if (n_rows == 0 || x_rows == 0) return DOL_OK;
+  if (!rowptr || !ent || !hdr) return fail(DOL_EINVAL, "dol_csr_slab_pack: null pointer");
+  const int nk = dol_csr_slab_nk(x_rows);
+  const int64_t len = dol_csr_slab_hdr_len(n_rows, x_rows);
+  if (cdiv(len, 256) >= (int64_t(1) << 31)) return fail(DOL_EINVAL, "dol_csr_slab_pack: too many chunk blocks");
+  hipLaunchKernelGGL(slab_count_kernel, dim3(static_cast<unsigned>(cdiv(len, 256))), dim3(256), 0, s, rowptr, col,
+                     n_rows, nk, len, hdr);
+  hipLaunchKernelGGL(slab_scan_kernel, dim3(1), dim3(1024), 0, s, hdr, len);
+  hipLaunchKernelGGL(slab_scatter_kernel, dim3(static_cast<unsigned>(n_rows)), dim3(64), 0, s, rowptr, col, val, nk,
+                     hdr, ent);
+  return dol::check_launch("dol_csr_slab_pack");
+}
+
+extern "C" int dol_dense_to_csr_f32(const float* W, int64_t ldw, int32_t n_rows, int32_t n_cols, int32_t* rowptr,
+                                    int32_t* col, float* val, int64_t cap, hipStream_t s) {
+  DOL_DIMS_OK("dol_dense_to_csr_f32", ldw, cap);
+  using dol::fail;
+  if (n_rows < 0 || n_cols < 0) return fail(DOL_EINVAL, "dol_dense_to_csr_f32: negative size");
+  if (!rowptr) return fail(DOL_EINVAL, "dol_dense_to_csr_f32: null rowptr");
+  if (int64_t(n_rows) * n_cols > int64_t(INT32_MAX)) return fail(DOL_EINVAL, "dol_dense_to_csr_f32: n_rows * n_cols >= 2^31");
+  if (n_rows > 0 && n_cols > 0 && (!W || !col || !val)) return fail(DOL_EINVAL, "dol_dense_to_csr_f32: null pointer");
+  if (n_rows > 0 && n_cols > 0 && ldw < n_cols) return fail(DOL_EINVAL, "dol_dense_to_csr_f32: ldw < n_cols");
+  if (cap < int64_t(n_rows) * n_cols)
+    return fail(DOL_EINVAL, "dol_dense_to_csr_f32: col/val capacity %lld < n_rows * n_cols", static_cast<long long>(cap));
+  if (n_rows == 0) return hipMemsetAsync(rowptr, 0, 4, s) == hipSuccess ? DOL_OK : fail(DOL_EINVAL, "memset failed");
+  if (n_cols == 0)
+    return hipMemsetAsync(rowptr, 0, (int64_t(n_rows) + 1) * 4, s) == hipSuccess ? DOL_OK
+           : fail(DOL_EINVAL, "dol_dense_to_csr_f32: memset failed");
+  hipLaunchKernelGGL(dense_count_kernel, dim3(n_rows), dim3(kRowThreads), 0, s, W, ldw, n_cols, rowptr);
+  hipLaunchKernelGGL(rowptr_scan_kernel, dim3(1), dim3(1024), 0, s, rowptr, n_rows);
+  hipLaunchKernelGGL(dense_fill_kernel, dim3(n_rows), dim3(kRowThreads), 0, s, W, ldw, n_cols, rowptr, col, val);
+  return dol::check_launch("dol_dense_to_csr_f32");
+}

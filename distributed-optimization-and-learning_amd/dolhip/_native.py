@@ -64,11 +64,18 @@ SIGNATURES = {
     "dol_dgd_csr_pm_f32": [_ptr, _i64, _i32, _ptr, _i64, _i32, _i64, _ptr, _ptr, _ptr, _ptr, _i64, _ptr, _i64, _i32,
                            _i32, _f32, _f32, ctypes.c_int, _ptr],
     "dol_transpose_f32": [_ptr, _i64, _ptr, _i64, _i64, _i64, _ptr],
+    "dol_csr_slab_nk": [_i32],
+    "dol_csr_slab_hdr_len": [_i32, _i32],
+    "dol_csr_slab_ent_len": [_i64],
+    "dol_mix_csr_slab_f32": [_ptr, _i64, _i32, _ptr, _i64, _i32, _i64, _ptr, _ptr, _ptr],
+    "dol_csr_slab_pack": [_ptr, _ptr, _ptr, _i32, _i32, _ptr, _ptr, _ptr],
+    "dol_dense_to_csr_f32": [_ptr, _i64, _i32, _i32, _ptr, _ptr, _ptr, _i64, _ptr],
 }
 _RESTYPES = {"dol_last_error": ctypes.c_char_p, "dol_admm_dual_workspace_bytes": ctypes.c_int64,
              "dol_admm_ls_round_workspace_bytes": ctypes.c_int64,
              "dol_mlp_step_lds_bytes": ctypes.c_int64, "dol_mlp_step_workspace_bytes": ctypes.c_int64,
-             "dol_mix_dense_split3_workspace_bytes": ctypes.c_int64}
+             "dol_mix_dense_split3_workspace_bytes": ctypes.c_int64, "dol_csr_slab_hdr_len": ctypes.c_int64,
+             "dol_csr_slab_ent_len": ctypes.c_int64}
 
 _lib = None
 

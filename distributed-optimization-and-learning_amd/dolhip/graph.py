@@ -339,13 +339,17 @@ class MixingPlan:
     """Device form of one W: CSR tensors plus the ring specialisation if it applies."""
 
     DENSE_KERNELS = ("split3", "f32")
+    SLAB_MIN_DEGREE = 16  # mean neighbours per row from which the LDS-gather CSR kernel takes over
 
     def __init__(self, csr: CSR, device, allow_ring: bool = True, dense: bool = False,
-                 dense_kernel: str = "split3"):
+                 dense_kernel: str = "split3", slab: Optional[bool] = None):
         """kind: 'ring' (bit-exact, ring kernel), 'csr' (bit-exact, any W), or
         'dense' (opt-in tolerance path: a GEMM over the dense W on the matrix
         cores; dense_kernel 'split3' = three-piece bf16 split at fp32 accuracy,
-        'f32' = exact-f32 MFMA fma chain)."""
+        'f32' = exact-f32 MFMA fma chain).  A 'csr' plan whose rows average at
+        least SLAB_MIN_DEGREE neighbours (or slab=True) also packs the CSR for
+        the LDS-gather kernel (dol_mix_csr_slab_f32, same bits), used whenever
+        the matrices' layout allows it."""
         if dense_kernel not in self.DENSE_KERNELS:
             raise ValueError(f"dense_kernel must be one of {self.DENSE_KERNELS}")
         self.dense_kernel = dense_kernel
@@ -353,6 +357,7 @@ class MixingPlan:
         self.csr = csr.validate()
         self.device = torch.device(device)
         self.n_rows = csr.n_rows
+        self.n_cols = csr.n_cols
         self.rowptr = torch.from_numpy(csr.rowptr).to(self.device)
         self.col = torch.from_numpy(csr.col).to(self.device)
         self.val = torch.from_numpy(csr.val).to(self.device)
@@ -364,6 +369,12 @@ class MixingPlan:
         if dense:
             # the CSR's selection (W_ij > 0 kept, NaN/negatives dropped) densified
             self.W = torch.from_numpy(csr.dense()).to(self.device)
+        self.ent = self.hdr = None
+        if slab is None:
+            slab = csr.nnz >= self.SLAB_MIN_DEGREE * max(1, csr.n_rows)
+        if self.kind == "csr" and slab and csr.n_rows > 0:
+            from . import ops
+            self.ent, self.hdr = ops.csr_slab_pack(self.rowptr, self.col, self.val, self.n_cols)
 
     @property
     def density(self) -> float:
@@ -372,21 +383,37 @@ class MixingPlan:
         return self.csr.nnz / max(1, self.csr.n_rows * self.csr.n_cols)
 
     @classmethod
-    def from_dense(cls, W: torch.Tensor, dense_kernel: str = "split3") -> "MixingPlan":
-        """A 'dense' plan straight from a device W (no CSR; e.g. a per-round
-        erdos_renyi_stochastic draw).  Only apply() (matrix cores) is available."""
+    def from_dense(cls, W: torch.Tensor, dense_kernel: str = "split3",
+                   reuse: Optional["MixingPlan"] = None) -> "MixingPlan":
+        """A plan straight from a device W (no host round trip; e.g. a per-round
+        erdos_renyi_stochastic_hip draw).  dense_kernel 'split3' / 'f32': a
+        'dense' plan on the matrix cores (tolerance path).  dense_kernel 'csr':
+        the Neighbors selection runs on the device (dol_dense_to_csr_f32) and
+        the plan mixes bit-exactly with the LDS-gather CSR kernel; `reuse` (a
+        previous 'csr' plan of the same shape) lends its buffers."""
         if W.device.type != "cuda" or W.dtype != torch.float32 or W.dim() != 2:
             raise ValueError("from_dense: expected a 2-D float32 CUDA tensor")
-        if dense_kernel not in cls.DENSE_KERNELS:
-            raise ValueError(f"dense_kernel must be one of {cls.DENSE_KERNELS}")
+        if dense_kernel not in cls.DENSE_KERNELS + ("csr",):
+            raise ValueError(f"dense_kernel must be one of {cls.DENSE_KERNELS + ('csr',)}")
         plan = cls.__new__(cls)
         plan.dense_kernel = dense_kernel
         plan._work, plan._work_key = None, None
         plan.csr = None
         plan.device = W.device
-        plan.n_rows = W.shape[0]
-        plan.kind = "dense"
+        plan.n_rows, plan.n_cols = W.shape
         plan.W = W.contiguous()
+        plan.ent = plan.hdr = None
+        if dense_kernel != "csr":
+            plan.kind = "dense"
+            return plan
+        from . import ops
+        plan.kind = "csr"
+        same = (reuse is not None and reuse.kind == "csr" and reuse.csr is None and reuse.device == W.device
+                and (reuse.n_rows, reuse.n_cols) == (plan.n_rows, plan.n_cols))
+        bufs = (reuse.rowptr, reuse.col, reuse.val) if same else (None, None, None)
+        plan.rowptr, plan.col, plan.val = ops.dense_to_csr(plan.W, *bufs)
+        plan.ent, plan.hdr = ops.csr_slab_pack(plan.rowptr, plan.col, plan.val, plan.n_cols,
+                                               *((reuse.ent, reuse.hdr) if same else (None, None)))
         return plan
 
     @classmethod
@@ -427,7 +454,7 @@ class MixingPlan:
         return 1
 
     def _check_x(self, X: torch.Tensor) -> None:
-        need = self.csr.n_cols if self.csr is not None else self.W.shape[1]
+        need = self.n_cols
         if X.shape[0] < need:
             raise ValueError(f"X has {X.shape[0]} rows; W has {need} columns")
 
@@ -438,6 +465,9 @@ class MixingPlan:
             return ops.mix_ring(X, Y, self.w_prev, self.w_next, P=P, n_rows=self.n_rows)
         if self.kind == "dense":
             return self._mix_dense(X, Y, P)
+        P_ = X.shape[1] if P is None else P
+        if self.ent is not None and ops.slab_layout_ok(X, Y, P_):
+            return ops.mix_csr_slab(X, Y, self.ent, self.hdr, self.n_rows, x_rows=self.n_cols, P=P_)
         return ops.mix_csr(X, Y, self.rowptr, self.col, self.val, P=P)
 
 

@@ -19,6 +19,7 @@ __all__ = [
     "ordered_sum", "stream_copy", "dual_workspace_bytes", "prox_grad", "admm_step_dual", "mlp_step",
     "dgd_ring", "dgd_csr", "OBJECTIVES", "admm_ls_round", "admm_ls_round_workspace_bytes", "mix_csr_pm",
     "transpose", "PM_MAX_AGENTS", "stream_copy_rows", "dgd_csr_pm", "PM_DGD_MAX_AGENTS",
+    "SLAB_CHUNK", "SLAB_ROWS", "csr_slab_pack", "mix_csr_slab", "slab_layout_ok", "dense_to_csr",
 ]
 
 PM_MAX_AGENTS = 8192  # dol_mix_csr_pm_f32: one p-row image (<= 32 KiB) per LDS stage
@@ -109,6 +110,101 @@ def mix_csr_pm(XT: torch.Tensor, YT: torch.Tensor, rowptr: torch.Tensor, col: to
     _native.call("dol_mix_csr_pm_f32", XT.data_ptr(), ldx, x_agents, YT.data_ptr(), ldy, n, P, rowptr.data_ptr(),
                  col.data_ptr() if col.numel() else None, val.data_ptr() if val.numel() else None, _stream(XT))
     return YT
+
+
+SLAB_CHUNK = 64  # DOL_SLAB_CHUNK: agents per LDS chunk of dol_mix_csr_slab_f32
+
+
+def _check_csr(rowptr: torch.Tensor, col: torch.Tensor, val: torch.Tensor, device) -> None:
+    for nm, t, dt in (("rowptr", rowptr, torch.int32), ("col", col, torch.int32), ("val", val, torch.float32)):
+        if t.device != device or t.dtype != dt or not t.is_contiguous():
+            raise ValueError(f"{nm}: expected contiguous {dt} on {device}")
+    if col.numel() != val.numel():
+        raise ValueError("col and val lengths differ")
+
+
+SLAB_ROWS = 128  # DOL_SLAB_ROWS: rows per row group of the chunk-major packing
+
+
+def csr_slab_pack(rowptr: torch.Tensor, col: torch.Tensor, val: torch.Tensor, x_rows: int,
+                  ent: Optional[torch.Tensor] = None, hdr: Optional[torch.Tensor] = None):
+    """(ent, hdr) of a device CSR for mix_csr_slab (dol_csr_slab_pack): the
+    entries re-packed chunk-major per group of SLAB_ROWS rows as (LDS byte
+    offset, weight bits) pairs, hdr[g][k][i] = first entry of row g*ROWS+i in
+    chunk k.  col/val may be longer than nnz (a capacity); ent is sized from it."""
+    n = rowptr.numel() - 1
+    _check_csr(rowptr, col, val, rowptr.device)
+    L = _native.lib()
+    need_e = int(L.dol_csr_slab_ent_len(col.numel()))
+    need_h = int(L.dol_csr_slab_hdr_len(n, int(x_rows)))
+    if ent is None or ent.numel() < need_e:
+        ent = torch.empty(max(need_e, 4), dtype=torch.int32, device=rowptr.device)
+    if hdr is None or hdr.numel() < need_h:
+        hdr = torch.empty(max(need_h, 4), dtype=torch.int32, device=rowptr.device)
+    _native.call("dol_csr_slab_pack", rowptr.data_ptr(), col.data_ptr() if col.numel() else None,
+                 val.data_ptr() if val.numel() else None, n, int(x_rows), ent.data_ptr(), hdr.data_ptr(),
+                 _stream(rowptr))
+    return ent, hdr
+
+
+def slab_layout_ok(X: torch.Tensor, Y: torch.Tensor, P: int) -> bool:
+    """Whether mix_csr_slab accepts these matrices: 16-B aligned rows, row
+    strides multiples of 4, X rows readable up to round_up(P, 4) floats."""
+    if X.dim() != 2 or Y.dim() != 2 or X.data_ptr() % 16 or Y.data_ptr() % 16:
+        return False
+    ldx = X.stride(0) if X.shape[0] > 1 else X.shape[1]
+    ldy = Y.stride(0) if Y.shape[0] > 1 else Y.shape[1]
+    p4 = -(-P // 4) * 4
+    if ldx % 4 or ldy % 4 or ldx < p4:
+        return False
+    need = X.storage_offset() + (X.shape[0] - 1) * ldx + p4
+    return need * 4 <= X.untyped_storage().nbytes()
+
+
+def mix_csr_slab(X: torch.Tensor, Y: torch.Tensor, ent: torch.Tensor, hdr: torch.Tensor, n_rows: int,
+                 x_rows: Optional[int] = None, P: Optional[int] = None) -> torch.Tensor:
+    """mix_csr for high-degree graphs (dol_mix_csr_slab_f32): the same sum in
+    the same order, bit-identical, with X's columns staged through LDS.
+    (ent, hdr) from csr_slab_pack.  Reference: DIST/simulators.py:91-97 +
+    DIST/clients.py:61-69."""
+    P = X.shape[1] if P is None else P
+    x_rows = X.shape[0] if x_rows is None else int(x_rows)
+    ldx = _check_rows("X", X, P)
+    ldy = _check_rows("Y", Y, P)
+    if Y.shape[0] < n_rows or X.shape[0] < x_rows:
+        raise ValueError(f"X has {X.shape[0]} rows (need {x_rows}), Y {Y.shape[0]} (need {n_rows})")
+    if not slab_layout_ok(X, Y, P):
+        raise ValueError("mix_csr_slab: X, Y need 16-B aligned rows with strides % 4 == 0 and X readable to "
+                         "round_up(P, 4) floats per row")
+    for nm, t in (("ent", ent), ("hdr", hdr)):
+        if t.device != X.device or t.dtype != torch.int32 or not t.is_contiguous():
+            raise ValueError(f"{nm}: expected contiguous int32 on {X.device}")
+    if hdr.numel() < int(_native.lib().dol_csr_slab_hdr_len(int(n_rows), x_rows)):
+        raise ValueError("hdr too short for these row counts (rebuild with csr_slab_pack)")
+    if X.data_ptr() == Y.data_ptr():
+        raise ValueError("X and Y alias: the Jacobi mix needs two buffers")
+    _native.call("dol_mix_csr_slab_f32", X.data_ptr(), ldx, x_rows, Y.data_ptr(), ldy, int(n_rows), P,
+                 ent.data_ptr(), hdr.data_ptr(), _stream(X))
+    return Y
+
+
+def dense_to_csr(W: torch.Tensor, rowptr: Optional[torch.Tensor] = None, col: Optional[torch.Tensor] = None,
+                 val: Optional[torch.Tensor] = None):
+    """Neighbors (DIST/simulators.py:91-97) of every row of a dense device W, on
+    the device (dol_dense_to_csr_f32): (rowptr, col, val) with col/val of
+    capacity n*m (nnz = rowptr[-1], not synchronised to the host)."""
+    ld = _check_rows("W", W)
+    n, m = W.shape
+    cap = n * m
+    if rowptr is None or rowptr.numel() < n + 1:
+        rowptr = torch.empty(n + 1, dtype=torch.int32, device=W.device)
+    if col is None or col.numel() < cap:
+        col = torch.empty(max(cap, 1), dtype=torch.int32, device=W.device)
+    if val is None or val.numel() < cap:
+        val = torch.empty(max(cap, 1), dtype=torch.float32, device=W.device)
+    _native.call("dol_dense_to_csr_f32", W.data_ptr(), ld, n, m, rowptr.data_ptr(), col.data_ptr(), val.data_ptr(),
+                 col.numel() if val.numel() >= col.numel() else val.numel(), _stream(W))
+    return rowptr, col, val
 
 
 def transpose(A: torch.Tensor, B: torch.Tensor, rows: Optional[int] = None, cols: Optional[int] = None) -> torch.Tensor:

@@ -74,6 +74,43 @@ int dol_mix_csr_pm_f32(const float* XT, int64_t ldx, int32_t x_rows, float* YT, 
                        int64_t P, const int32_t* rowptr, const int32_t* col, const float* val, hipStream_t s);
 
 /*
+ * dol_mix_csr_f32 for HIGH-DEGREE graphs (tens to thousands of neighbours per
+ * row: Erdos-Renyi, dense-ish time-varying W; BASELINE config 5), same
+ * reference code (DIST/simulators.py:91-97 + DIST/clients.py:61-69), same
+ * rounding, bit-identical results.  X's columns stream through LDS in chunks
+ * of DOL_SLAB_CHUNK agents; each row's neighbour sum is gathered from LDS in
+ * ascending column order.  The CSR comes re-packed chunk-major by
+ * dol_csr_slab_pack (rows in groups of DOL_SLAB_ROWS; for group g and chunk k
+ * the entries of the group's rows with columns in the chunk are contiguous):
+ *   ent  int32 [dol_csr_slab_ent_len(nnz)]: (LDS byte offset, weight bits) pairs
+ *   hdr  int32 [dol_csr_slab_hdr_len(n_rows, x_rows)]: hdr[g][k][i] = ent
+ *        index of row g*DOL_SLAB_ROWS+i's first entry in chunk k (i <= ROWS)
+ * Limits: ldx, ldy multiples of 4, ldx >= round_up(P, 4) (X rows readable in
+ * whole 16-B pieces), X, Y and ent 16-B aligned, X and Y not aliased.
+ */
+#define DOL_SLAB_CHUNK 64
+#define DOL_SLAB_ROWS 128
+int dol_csr_slab_nk(int32_t x_rows);
+int64_t dol_csr_slab_hdr_len(int32_t n_rows, int32_t x_rows);
+int64_t dol_csr_slab_ent_len(int64_t nnz_capacity);
+int dol_mix_csr_slab_f32(const float* X, int64_t ldx, int32_t x_rows, float* Y, int64_t ldy, int32_t n_rows,
+                         int64_t P, const int32_t* ent, const int32_t* hdr, hipStream_t s);
+/* ent and hdr (above) of a device CSR (rowptr / col / val as dol_mix_csr_f32,
+ * 0 <= col < x_rows); ent sized for the CSR's nnz (or a capacity >= nnz). */
+int dol_csr_slab_pack(const int32_t* rowptr, const int32_t* col, const float* val, int32_t n_rows,
+                      int32_t x_rows, int32_t* ent, int32_t* hdr, hipStream_t s);
+/*
+ * Neighbors (DIST/simulators.py:91-97) of every row of a dense device W, on
+ * the device: rowptr[n_rows + 1] and col / val (capacity cap >= n_rows *
+ * n_cols entries; nnz = rowptr[n_rows]) with the reference's selection
+ * (W_ij > 0, NaN and <= 0 dropped, j ascending): a W drawn every round
+ * (dol_er_stochastic_f32) becomes a CSR without a host round trip.
+ * n_rows * n_cols < 2^31.
+ */
+int dol_dense_to_csr_f32(const float* W, int64_t ldw, int32_t n_rows, int32_t n_cols, int32_t* rowptr,
+                         int32_t* col, float* val, int64_t cap, hipStream_t s);
+
+/*
  * B[c * ldb + r] = A[r * lda + c] for r < rows, c < cols (fp32, tiled through
  * LDS): converts the agent-major bank to the parameter-major one and back
  * (setup and checkpoint time, not on the round path).  A and B must not alias.

@@ -60,6 +60,32 @@ def test_argument_errors_are_reported_without_launch():
     assert rc == -1 and b"workspace" in L.dol_last_error()
 
 
+def test_slab_entry_points_check_arguments():
+    L = _native.lib()
+    fake = 1 << 20  # never dereferenced
+    assert L.dol_csr_slab_nk(1024) == 16 and L.dol_csr_slab_nk(65) == 2 and L.dol_csr_slab_nk(0) == 0
+    assert L.dol_csr_slab_hdr_len(1000, 1024) == 8 * 16 * 129
+    assert L.dol_csr_slab_ent_len(100) == 2 * (100 + 160)
+    rc = L.dol_mix_csr_slab_f32(fake, 16, 8, fake, 16, 8, 16, None, fake, None)
+    assert rc == -1 and b"null pointer" in L.dol_last_error()
+    rc = L.dol_mix_csr_slab_f32(fake, 16, 8, fake, 16, 8, 16, fake, fake, None)
+    assert rc == -1 and b"alias" in L.dol_last_error()
+    rc = L.dol_mix_csr_slab_f32(fake, 18, 8, fake + 4096, 16, 8, 16, fake, fake, None)
+    assert rc == -1 and b"multiples of 4" in L.dol_last_error()
+    rc = L.dol_mix_csr_slab_f32(fake, 16, 8, fake + 4096, 16, 8, 15, fake + 8, fake, None)
+    assert rc == -1 and b"aligned" in L.dol_last_error()
+    rc = L.dol_mix_csr_slab_f32(fake + 4, 16, 8, fake + 4096, 16, 8, 16, fake, fake, None)
+    assert rc == -1 and b"16-B aligned" in L.dol_last_error()
+    rc = L.dol_dense_to_csr_f32(fake, 8, 8, 8, fake, fake, fake, 63, None)
+    assert rc == -1 and b"capacity" in L.dol_last_error()
+    rc = L.dol_dense_to_csr_f32(fake, 4, 8, 8, fake, fake, fake, 64, None)
+    assert rc == -1 and b"ldw" in L.dol_last_error()
+    rc = L.dol_dense_to_csr_f32(fake, 70000, 70000, 70000, fake, fake, fake, 1 << 40, None)
+    assert rc == -1 and b"2^31" in L.dol_last_error()
+    rc = L.dol_csr_slab_pack(None, fake, fake, 8, 8, fake, fake, None)
+    assert rc == -1 and b"null pointer" in L.dol_last_error()
+
+
 def test_split3_workspace_sizes():
     L = _native.lib()
     full = L.dol_mix_dense_split3_workspace_bytes(1024, 1024, 101770, 0)
