@@ -281,6 +281,51 @@ def dense_mix_round(device, N: int = 1024, P: int = 101770, reps: int = 10):
                     "split pass included"}
 
 
+def er_exact_mix_round(device, N: int = 1024, P: int = 101770, reps: int = 10):
+    """Secondary (BASELINE config 5's mixing, N = 1), bit-exact: the same
+    Erdos-Renyi p = 0.1 W drawn on the device each round (dol_er_stochastic_f32),
+    its Neighbors selection on the device (dol_dense_to_csr_f32 + the
+    chunk-major packing) and the LDS-gather CSR mix (dol_mix_csr_slab_f32) --
+    the reference's consensus bit for bit; draw + CSR build included in the
+    round time, the mix kernel timed separately."""
+    from dolhip import graph as G
+    from dolhip.bank import row_stride
+    gen = torch.Generator(device=device).manual_seed(2028)
+    X = torch.empty(N, row_stride(P), device=device).normal_(generator=gen)
+    Y = torch.empty_like(X)
+    Wbuf = torch.empty(N, N, device=device)
+    st = {"plan": None, "r": 0}
+
+    def draw():
+        st["r"] += 1
+        W = G.erdos_renyi_stochastic_hip(N, 0.1, 2028 * 1000003 + st["r"], device, out=Wbuf)
+        st["plan"] = G.MixingPlan.from_dense(W, dense_kernel="csr", reuse=st["plan"])
+    draw()
+    st["plan"].apply(X, Y, P=P)
+    torch.cuda.synchronize(device)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    ev[0].record()
+    for _ in range(reps):
+        draw()
+        st["plan"].apply(X, Y, P=P)
+    ev[1].record()
+    ev[2].record()
+    for _ in range(reps):
+        st["plan"].apply(X, Y, P=P)
+    ev[3].record()
+    torch.cuda.synchronize(device)
+    ms_round = ev[0].elapsed_time(ev[1]) / reps
+    ms_mix = ev[2].elapsed_time(ev[3]) / reps
+    nnz = int(st["plan"].rowptr[-1].item())
+    del X, Y, Wbuf, st
+    torch.cuda.empty_cache()
+    return {"agents": N, "params": P, "nnz": nnz, "ms_per_round": ms_round, "rounds_per_s": 1e3 / ms_round,
+            "mix_ms": ms_mix, "lds_GBps": nnz * P * 4 / (ms_mix / 1e3) / 1e9,
+            "kernel": "csr_slab_kernel (LDS-gather CSR) + dense_to_csr + slab_pack",
+            "what": "the same time-varying ER p=0.1 W as dense_er_mix, mixed bit-exactly (reference consensus order); "
+                    "W draw + device Neighbors + packing included in ms_per_round"}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -384,9 +429,10 @@ def main():
     if not args.no_primal_dual:
         pd_round = primal_dual_round(N, P, world, rank, device, args.pd_steps)
     _log("primal/dual round done")
-    dense = None
+    dense = exact = None
     if world == 1 and not args.no_primal_dual:
         dense = dense_mix_round(device)
+        exact = er_exact_mix_round(device)
     _log("dense ER done")
 
     traffic = None
@@ -451,6 +497,7 @@ def main():
             "fedlcon_eps5": fedlcon,
             "random_regular_pm": rr_pm,
             "dense_er_mix": dense,
+            "er_exact_mix": exact,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -69,13 +69,17 @@ struct I2 {
   int32_t x, y;  // (LDS byte offset of the neighbour's piece in its chunk, weight bits)
 };
 
-__device__ __forceinline__ f4 fmac(f4 acc, float w, f4 x) {  // separately rounded mul, then add
-  return acc + x * w;
-}
+// separately rounded mul, then add (v_pk_mul_f32 / v_pk_add_f32 pairs: 1.18 ms
+// vs 1.33 with the per-component scalar form at 1024 x 101,770, same bits)
+__device__ __forceinline__ f4 fmac(f4 acc, float w, f4 x) { return acc + x * w; }
 
 // PROBE (diagnostics, DOL_SLAB_PROBE): 1 = staging only (no gathers), 2 = gathers
 // only (no LDS-DMA: sums of whatever LDS holds; results meaningless).
-template <int PROBE = 0>
+// BCAST (default): each neighbour's (offset, weight) by a uniform LDS read
+// (ds_read2_b64 for two) into VGPRs; otherwise (DOL_SLAB_READLANE=1) by
+// v_readlane from the group's lane-distributed index: 1.12 vs 1.17 ms at
+// 1024 x 101,770 (profiles/r02_slab_probe.txt).
+template <int PROBE = 0, bool BCAST = true>
 __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
     const float* __restrict__ X, int64_t ldx, int x_rows, float* __restrict__ Y, int64_t ldy, int n_rows, int64_t P,
     const int32_t* __restrict__ ent, const int32_t* __restrict__ hdr, int nk, int n_rg, int64_t n_slabs) {
@@ -161,34 +165,56 @@ __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
       }
       const I2 q = *reinterpret_cast<const I2*>(ib + 8 * min(gs + lane, ge - 1));
       const int vo = q.x, vw = q.y;
+      // entry j of the group: (LDS byte offset, weight); the lane-distributed
+      // copy (vo, vw) is only read in the v_readlane variant
+      auto ent_at = [&](int j, uint32_t& o, float& w) {
+        if constexpr (BCAST) {
+          const I2 e = *reinterpret_cast<const I2*>(ib + 8 * (gs + j));
+          o = uint32_t(e.x);
+          w = __int_as_float(e.y);
+        } else {
+          o = uint32_t(__builtin_amdgcn_readlane(vo, j));
+          w = __int_as_float(__builtin_amdgcn_readlane(vw, j));
+        }
+      };
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int j1 = bnd[4 * g + i + 1] - gs;
         int j = bnd[4 * g + i] - gs;
         f4 a = acc[4 * g + i];
         for (; j + 4 <= j1; j += 4) {
-          const uint32_t o0 = __builtin_amdgcn_readlane(vo, j), o1 = __builtin_amdgcn_readlane(vo, j + 1);
-          const uint32_t o2 = __builtin_amdgcn_readlane(vo, j + 2), o3 = __builtin_amdgcn_readlane(vo, j + 3);
+          uint32_t o0, o1, o2, o3;
+          float w0, w1, w2, w3;
+          ent_at(j, o0, w0);
+          ent_at(j + 1, o1, w1);
+          ent_at(j + 2, o2, w2);
+          ent_at(j + 3, o3, w3);
           const f4 x0 = *reinterpret_cast<const f4*>(lds + xbase + o0);
           const f4 x1 = *reinterpret_cast<const f4*>(lds + xbase + o1);
           const f4 x2 = *reinterpret_cast<const f4*>(lds + xbase + o2);
           const f4 x3 = *reinterpret_cast<const f4*>(lds + xbase + o3);
-          a = fmac(a, __int_as_float(__builtin_amdgcn_readlane(vw, j)), x0);
-          a = fmac(a, __int_as_float(__builtin_amdgcn_readlane(vw, j + 1)), x1);
-          a = fmac(a, __int_as_float(__builtin_amdgcn_readlane(vw, j + 2)), x2);
-          a = fmac(a, __int_as_float(__builtin_amdgcn_readlane(vw, j + 3)), x3);
+          a = fmac(a, w0, x0);
+          a = fmac(a, w1, x1);
+          a = fmac(a, w2, x2);
+          a = fmac(a, w3, x3);
         }
         if (j + 2 <= j1) {
-          const uint32_t o0 = __builtin_amdgcn_readlane(vo, j), o1 = __builtin_amdgcn_readlane(vo, j + 1);
+          uint32_t o0, o1;
+          float w0, w1;
+          ent_at(j, o0, w0);
+          ent_at(j + 1, o1, w1);
           const f4 x0 = *reinterpret_cast<const f4*>(lds + xbase + o0);
           const f4 x1 = *reinterpret_cast<const f4*>(lds + xbase + o1);
-          a = fmac(a, __int_as_float(__builtin_amdgcn_readlane(vw, j)), x0);
-          a = fmac(a, __int_as_float(__builtin_amdgcn_readlane(vw, j + 1)), x1);
+          a = fmac(a, w0, x0);
+          a = fmac(a, w1, x1);
           j += 2;
         }
-        if (j < j1)
-          a = fmac(a, __int_as_float(__builtin_amdgcn_readlane(vw, j)),
-                   *reinterpret_cast<const f4*>(lds + xbase + uint32_t(__builtin_amdgcn_readlane(vo, j))));
+        if (j < j1) {
+          uint32_t o0;
+          float w0;
+          ent_at(j, o0, w0);
+          a = fmac(a, w0, *reinterpret_cast<const f4*>(lds + xbase + o0));
+        }
         acc[4 * g + i] = a;
       }
     }
@@ -402,8 +428,10 @@ extern "C" int dol_mix_csr_slab_f32(const float* X, int64_t ldx, int32_t x_rows,
     hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(grid)), dim3(kThreads), kLds, s, X, ldx, x_rows, Y, ldy,
                        n_rows, P, ent, hdr, nk, static_cast<int>(n_rg), n_slabs);
   };
+  static const bool readlane = [] { const char* e = getenv("DOL_SLAB_READLANE"); return e && atoi(e) != 0; }();
   if (probe == 1) launch(csr_slab_kernel<1>);
   else if (probe == 2) launch(csr_slab_kernel<2>);
+  else if (readlane) launch(csr_slab_kernel<0, false>);
   else launch(csr_slab_kernel<0>);
   return dol::check_launch("dol_mix_csr_slab_f32");
 }

@@ -32,10 +32,12 @@ def time_plan(plan, X, Y, P, reps):
     return s.elapsed_time(e) / reps
 
 
-def mlp_round(N, d, h, c, B, p_edge, reps, dev):
+def mlp_round(N, d, h, c, B, p_edge, reps, dev, mix="split3"):
     """BASELINE config 5: a NEW Erdos-Renyi W every round (drawn on the device,
-    graph.erdos_renyi_stochastic_hip), mixed on the dense matrix-core path, then one
-    fused local step of every agent's MLP (dol_mlp_step_f32)."""
+    graph.erdos_renyi_stochastic_hip), mixed on the dense matrix-core path
+    (mix='split3') or bit-exactly by the LDS-gather CSR kernel after a device
+    Neighbors pass (mix='csr'), then one fused local step of every agent's MLP
+    (dol_mlp_step_f32)."""
     from dolhip.bank import AgentBank
     from dolhip.mlp import BatchedMLP, mlp_layout
     bank = AgentBank(N, mlp_layout(d, h, c), dev)
@@ -49,7 +51,10 @@ def mlp_round(N, d, h, c, B, p_edge, reps, dev):
     def draw():  # a new W every round: one HIP kernel (graph_draw.hip), seeded per round
         state["round"] += 1
         W = G.erdos_renyi_stochastic_hip(N, p_edge, 2028 * 1000003 + state["round"], dev, out=state["W"])
-        state["plan"] = G.MixingPlan.from_dense(W)
+        if mix == "csr":
+            state["plan"] = G.MixingPlan.from_dense(W, dense_kernel="csr", reuse=state.get("plan"))
+        else:
+            state["plan"] = G.MixingPlan.from_dense(W)
     X = torch.randn(N, B, d, device=dev)
     y = torch.randint(0, c, (N, B), device=dev)
     ev = {k: [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
@@ -102,8 +107,9 @@ def mlp_round(N, d, h, c, B, p_edge, reps, dev):
     P = bank.P
     flops_fb = 2.0 * N * B * (d * h + h * c) * 3  # fwd + two backward GEMMs per layer
     local_bytes = N * (4 * P + B * d) * 4           # w, mom in + out, X in (compulsory)
-    out = {"workload": "config5: time-varying ER p=%.2f (new W per round, on device) dense MFMA mix + fused MLP "
-                       "%d-%d-%d local step" % (p_edge, d, h, c),
+    out = {"workload": "config5: time-varying ER p=%.2f (new W per round, on device) %s mix + fused MLP "
+                       "%d-%d-%d local step" % (p_edge, "bit-exact LDS-gather CSR" if mix == "csr" else
+                                                "dense MFMA (split3)", d, h, c), "mix_path": mix,
            "agents": N, "params": P, "batch": B, "ms_per_round": el * 1e3, "rounds_per_s": 1 / el, "kernel_ms": ms,
            "mix_TFLOPs": 2.0 * N * N * P / (ms["mix"] / 1e3) / 1e12,
            "local_TFLOPs": flops_fb / (ms["local"] / 1e3) / 1e12,
@@ -232,6 +238,7 @@ def main():
     ap.add_argument("--topologies", nargs="+", default=["ring", "ring-eps5", "rr4", "dense-er0.1"])
     ap.add_argument("--dense-max-agents", type=int, default=2048)
     ap.add_argument("--mlp", type=int, nargs="*", default=[1024], help="agent counts for the config-5 MLP round")
+    ap.add_argument("--mlp-mix", nargs="+", default=["split3", "csr"], help="config-5 mix paths")
     ap.add_argument("--dgd", type=int, nargs="*", default=[1024], help="agent counts for the config-3 DGD round")
     ap.add_argument("--dgd-topologies", nargs="+", default=["ring", "rr4"])
     ap.add_argument("--dgd-pm", type=int, nargs="*", default=[1024],
@@ -240,7 +247,8 @@ def main():
     dev = torch.device("cuda")
     P = a.params
     for N in a.mlp:
-        mlp_round(N, 784, 128, 10, 32, 0.1, a.reps, dev)
+        for mix in a.mlp_mix:
+            mlp_round(N, 784, 128, 10, 32, 0.1, a.reps, dev, mix=mix)
     for N in a.dgd:
         for topo in a.dgd_topologies:
             dgd_round(N, P, topo, "least_squares", 0.5, 1, a.reps, dev)
