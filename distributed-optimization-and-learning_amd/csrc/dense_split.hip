@@ -26,10 +26,12 @@
 // register round trip, no bounds checks) and reads fragments conflict-free
 // (48-B lane stride).
 //
-// GEMM.  256 x 256 output tile per workgroup, 4 waves in 2 x 2, each wave
-// 128 x 128 = 4 x 4 accumulators of 32 x 32 (256 accumulator registers, one
-// wave per SIMD).  K advances 16 per stage (= one MFMA k-step); three stages
-// of 48 KiB in LDS, two in flight while one feeds 96 MFMAs per wave.  Tile
+// GEMM.  256 x 256 output tile per workgroup, 8 waves in 2 x 4, each wave
+// 128 x 64 = 4 x 2 accumulators of 32 x 32 (128 accumulator registers, two
+// waves per SIMD; the r01 form, 4 waves of 128 x 128 with 256 accumulator
+// registers, remains for the narrow tail tiles and DOL_SPLIT3_WAVES=4).
+// K advances 16 per stage (= one MFMA k-step); three stages of 48 KiB in LDS,
+// two in flight while one feeds 48 MFMAs per wave.  Tile
 // order is XCD-aware: workgroup b runs on XCD b % 8, each XCD walks a
 // contiguous range of tiles in groups of 8 row tiles, so the 32 tiles an XCD
 // holds at once share 8 W panels and 4 X panels in its L2.
@@ -133,15 +135,13 @@ __global__ __launch_bounds__(256) void split3_cols_kernel(const float* __restric
   write_record(v, out + idx * kRec);
 }
 
-template <bool FX, int NB = 4>
-__device__ __forceinline__ void wait_vmcnt_stage(bool more) {
+// wait until at most N of this wave's vector-memory operations are in flight
+template <int N>
+__device__ __forceinline__ void wait_vmcnt_le(bool more) {
   if (!more) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  else if (FX) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // kDmaFX: the next stage may fly
-  else if (NB == 1) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");  // 30 DMAs over 4 waves: 7 or 8 each
-  else if (NB == 2) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");  // 36 DMAs: 9 each
-  else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");          // kDmaPerWave
+  else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
-static_assert(kDmaPerWave == 12 && kDmaFX == 10, "wait_vmcnt_stage assumes 12 / 10 DMA instructions per wave");
+static_assert(kDmaPerWave == 12 && kDmaFX == 10, "stage sizes changed: recheck the DMA counts per wave");
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
@@ -210,27 +210,35 @@ __device__ __forceinline__ void split8(const float (&v)[8], bf16x8& p0, bf16x8& 
 // the last, partial wave of tiles on four / two times as many CUs.  Every output
 // element sees the same k-steps and the same six MFMAs in the same order
 // under either width, so the two are bit-identical.
-template <int PROBE, bool FX, int NB = 4>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+// WN: waves along P (2 x WN waves).  WN = 2: 4 waves, one per SIMD, 128 x 32 NB
+// each (DOL_SPLIT3_WAVES=4, and the narrow tail tiles); WN = 4 (with NB = 2, the
+// default for 256 x 256 tiles): 8 waves, two per SIMD, 128 x 64 each, so one
+// wave's LDS-DMA issue and fragment reads overlap the other's MFMAs.
+template <int PROBE, bool FX, int NB = 4, int WN = 2>
+__global__ __launch_bounds__(128 * WN) __attribute__((amdgpu_waves_per_eu(WN / 2, WN / 2)))
 void dense_split3_kernel(const uint8_t* __restrict__ WA, const uint8_t* __restrict__ XB, float* __restrict__ Y,
                          int64_t ldy, int M, int64_t P, int64_t Mp, int64_t Pp, int n_stages, int n_mt,
                          int64_t n_pt, int64_t tiles_per_xcd, int group_m, const float* __restrict__ X,
                          int64_t ldx, int K, int64_t pread, int64_t t_base, int64_t t_end) {
-  static_assert(NB == 4 || ((NB == 1 || NB == 2) && !FX && PROBE == 0), "narrow tiles: split-pass operands only");
-  constexpr int BN = 64 * NB;                              // tile width along P
+  static_assert((WN == 2 && (NB == 4 || ((NB == 1 || NB == 2) && !FX && PROBE == 0))) ||
+                    (WN == 4 && NB == 2 && !FX),
+                "tiles: 256 x 256 (4 or 8 waves) or narrow split-pass tiles");
+  constexpr int kWaves = 2 * WN;
+  constexpr int BN = 32 * NB * WN;                         // tile width along P
+  constexpr int kParts = kTile / BN;                       // narrow tiles per 256-wide tile
   constexpr int kStage = FX ? kStageFX : kOpStage + 2 * BN * kRec;
-  constexpr int kDmaTot = FX ? 4 * kDmaFX : 24 + 6 * NB;   // 1-KiB DMA pieces per stage
-  constexpr int kDma = (kDmaTot + 3) / 4;
+  constexpr int kDmaTot = FX ? 4 * kDmaFX : 24 + 3 * BN / 32;  // 1-KiB DMA pieces per stage
+  constexpr int kDma = (kDmaTot + kWaves - 1) / kWaves;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   int64_t t;
   int quarter = 0;
-  if constexpr (NB == 4) {
+  if constexpr (kParts == 1) {
     const int64_t j = blockIdx.x >> 3;
     t = (blockIdx.x & 7) * tiles_per_xcd + j;
     if (j >= tiles_per_xcd || t >= t_end) return;
   } else {
-    t = t_base + blockIdx.x / (4 / NB);
-    quarter = blockIdx.x % (4 / NB);
+    t = t_base + blockIdx.x / kParts;
+    quarter = blockIdx.x % kParts;
     if (t >= t_end) return;
   }
   const int64_t per_group = int64_t(group_m) * n_pt;
@@ -243,7 +251,7 @@ void dense_split3_kernel(const uint8_t* __restrict__ WA, const uint8_t* __restri
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WN, wn = wave % WN;
   const int h = lane >> 5, li = lane & 31;
 
   // stage s holds k-groups 2s, 2s+1 of both operands: [A kg0 | A kg1 | B kg0 | B kg1], 12 KiB each
@@ -256,9 +264,9 @@ void dense_split3_kernel(const uint8_t* __restrict__ WA, const uint8_t* __restri
     uint8_t* st = lds + (s % kStages) * kStage;
 #pragma unroll
     for (int i = 0; i < kDma; ++i) {
-      const int q = wave + 4 * i;      // 1 KiB each (A records) / one fp32 row of 256 p (FX B)
-      if (kDmaTot % 4 && q >= kDmaTot) continue;
-      if (!FX && NB != 4 && q >= 24) {  // narrow B: 3 * NB pieces per k-group
+      const int q = wave + kWaves * i;  // 1 KiB each (A records) / one fp32 row of 256 p (FX B)
+      if (kDmaTot % kWaves && q >= kDmaTot) continue;
+      if (!FX && kParts != 1 && q >= 24) {  // narrow B: 3 * NB pieces per k-group
         const int qb = q - 24, kgl = qb / (3 * NB), chunk = qb % (3 * NB);
         const uint8_t* src = srcB + (2 * int64_t(s) + kgl) * pitchB + chunk * 1024;
         __builtin_amdgcn_global_load_lds(DOL_GPTR(src), DOL_LPTR(st + q * 1024), 16, 0, 0);
@@ -344,7 +352,7 @@ void dense_split3_kernel(const uint8_t* __restrict__ WA, const uint8_t* __restri
   issue(0);
   if (n_stages > 1) issue(1);
   for (int s = 0; s < n_stages; ++s) {
-    wait_vmcnt_stage<FX, NB>(s + 1 < n_stages);  // my DMA of stage s landed
+    wait_vmcnt_le<kDmaTot / kWaves>(s + 1 < n_stages);  // my DMA of stage s landed (the fewest any wave issues)
     barrier();                           // ... and every wave's; stage (s + 2) % 3 is free
     if (s + 2 < n_stages) issue(s + 2);
     if constexpr (PROBE == 2) continue;
@@ -440,6 +448,10 @@ extern "C" int dol_mix_dense_split3_f32(const float* W, int64_t ldw, const float
   }
   // diagnostics knobs (tools/gpu_dense_probe.sh); read once per process
   static const int probe = [] { const char* e = getenv("DOL_SPLIT3_PROBE"); return e ? atoi(e) : 0; }();
+  // 8 waves (two per SIMD) unless DOL_SPLIT3_WAVES=4: 1.07-1.10 vs 1.11-1.12 ms at
+  // 1024 x 101,770, 54.4-54.5 vs 56.2 ms at 8192 (profiles/r02_split3_waves.txt);
+  // same bits (tests/test_kernels_gpu.py split3 tests under both)
+  static const bool waves8 = [] { const char* e = getenv("DOL_SPLIT3_WAVES"); return !(e && atoi(e) == 4); }();
   static const int group_m = [] {
     const char* e = getenv("DOL_SPLIT3_GROUP_M");
     return e && atoi(e) > 0 ? atoi(e) : kGroupM;
@@ -469,10 +481,10 @@ extern "C" int dol_mix_dense_split3_f32(const float* W, int64_t ldw, const float
   if (8 * tiles_per_xcd >= (int64_t(1) << 32) || 4 * tail >= (int64_t(1) << 32))
     return fail(DOL_EINVAL, "dol_mix_dense_split3_f32: too many tiles");
   const int64_t pread = (P % 4 == 0) ? P : (P + 3) / 4 * 4;
-  auto launch = [&](auto kern, int lds, int64_t grid, int64_t t_base, int64_t t_end) {
+  auto launch = [&](auto kern, int lds, int64_t grid, int64_t t_base, int64_t t_end, int threads = 256) {
     // > 64 KiB of dynamic LDS: set on every call (cheap), so every device of the process gets it
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(grid)), dim3(256), lds, s, wa, xb, Y, ldy, M,
+    hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(grid)), dim3(threads), lds, s, wa, xb, Y, ldy, M,
                        P, g.Mp, g.Pp, static_cast<int>(g.Kg / 2), n_mt, n_pt, tiles_per_xcd, group_m, X, ldx, K,
                        pread, t_base, t_end);
   };
@@ -486,6 +498,9 @@ extern "C" int dol_mix_dense_split3_f32(const float* W, int64_t ldw, const float
     else if (probe == 2) launch(dense_split3_kernel<2, false>, kLds, grid, 0, t_main);
     else if (probe == 3) launch(dense_split3_kernel<3, false>, kLds, grid, 0, t_main);
     else if (probe == 4) launch(dense_split3_kernel<4, false>, kLds, grid, 0, t_main);
+    else if (waves8 && probe == 0) launch(dense_split3_kernel<0, false, 2, 4>, kLds, grid, 0, t_main, 512);
+    else if (waves8 && probe == 5) launch(dense_split3_kernel<1, false, 2, 4>, kLds, grid, 0, t_main, 512);
+    else if (waves8 && probe == 6) launch(dense_split3_kernel<2, false, 2, 4>, kLds, grid, 0, t_main, 512);
     else launch(dense_split3_kernel<0, false>, kLds, grid, 0, t_main);
   }
   if (narrow_tail && nb_tail == 1)
