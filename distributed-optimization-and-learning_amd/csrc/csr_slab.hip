@@ -54,8 +54,12 @@ constexpr int kWaves = 16;
 constexpr int kThreads = 64 * kWaves;
 constexpr int kXBytes = kChunk * kCols * 4;  // 64 KiB of X per chunk
 constexpr int kIdxBytes = 16 * 1024;          // index block capacity per chunk (2048 entries)
-constexpr int kBuf = kXBytes + kIdxBytes;     // one stage
-constexpr int kLds = 2 * kBuf;                // double buffer: 160 KiB
+// LDS: X stage 0 at 0, X stage 1 at 64 KiB (bits 10-15 of both bases clear, so
+// one v_bfi_b32 merges a piece's offset, the stage base and the lane offset),
+// index stages at 128 KiB and 144 KiB: 160 KiB
+constexpr int kIdxBase = 2 * kXBytes;
+constexpr int kLds = 2 * kXBytes + 2 * kIdxBytes;
+constexpr uint32_t kPieceMask = 0xFC00u;       // bits of an entry's offset word that select the piece (agent)
 constexpr int kRW = 8;                        // rows per wave
 constexpr int kRows = kWaves * kRW;           // rows per row group
 constexpr int kEntPad = 160;                  // ent pad entries (the block DMA may read 1 KiB + 8 B past a block)
@@ -73,13 +77,21 @@ struct I2 {
 // vs 1.33 with the per-component scalar form at 1024 x 101,770, same bits)
 __device__ __forceinline__ f4 fmac(f4 acc, float w, f4 x) { return acc + x * w; }
 
+// LDS byte address of entry word `o`'s piece for this lane (stage base | lane * 16
+// in `lb`): one v_bfi_b32
+__device__ __forceinline__ uint32_t piece_addr(uint32_t o, uint32_t lb) { return (o & kPieceMask) | (lb & ~kPieceMask); }
+
 // PROBE (diagnostics, DOL_SLAB_PROBE): 1 = staging only (no gathers), 2 = gathers
 // only (no LDS-DMA: sums of whatever LDS holds; results meaningless).
-// BCAST (default): each neighbour's (offset, weight) by a uniform LDS read
-// (ds_read2_b64 for two) into VGPRs; otherwise (DOL_SLAB_READLANE=1) by
-// v_readlane from the group's lane-distributed index: 1.12 vs 1.17 ms at
-// 1024 x 101,770 (profiles/r02_slab_probe.txt).
-template <int PROBE = 0, bool BCAST = true>
+// MODE 1 (default): rows one by one in groups of 4 / 2 / 1 entries, each
+//   group's (offset, weight) pairs by uniform LDS reads (ds_read2_b64) into
+//   VGPRs; MODE 2 (DOL_SLAB_MODE=2): by v_readlane from the group's
+//   lane-distributed index.  1024 x 101,770: 1.12 vs 1.17 ms.  Tried and
+//   dropped (profiles/r02_slab_probe.txt): the wave's entries as one stream in
+//   windows of 4 / 8 across row boundaries, each entry's accumulator chosen by
+//   a uniform switch on a row tag (5.4 ms; needs 8 waves x 16 rows for
+//   registers, and those slow mode 1 to 1.5 ms); index by scalar loads (2.1 ms).
+template <int PROBE = 0, int MODE = 1>
 __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
     const float* __restrict__ X, int64_t ldx, int x_rows, float* __restrict__ Y, int64_t ldy, int n_rows, int64_t P,
     const int32_t* __restrict__ ent, const int32_t* __restrict__ hdr, int nk, int n_rg, int64_t n_slabs) {
@@ -99,7 +111,7 @@ __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
 
   auto issue = [&](int k) {
     if constexpr (PROBE == 2) return;
-    uint8_t* dst = lds + (k & 1) * kBuf;
+    uint8_t* dst = lds + (k & 1) * kXBytes;
 #pragma unroll
     for (int i = 0; i < kPerWave; ++i) {
       const int al = wave * kPerWave + i;
@@ -110,9 +122,10 @@ __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
     const int64_t e0 = H[int64_t(k) * (kRows + 1)], e1 = H[int64_t(k) * (kRows + 1) + kRows];
     const int64_t a0 = (e0 * 8) & ~int64_t(15);
     const int64_t nbytes = e1 * 8 - a0;
-    if (nbytes <= kIdxBytes && wave * 1024 < nbytes)
-      __builtin_amdgcn_global_load_lds(DOL_GPTR(entb + a0 + wave * 1024 + lane * 16),
-                                       DOL_LPTR(dst + kXBytes + wave * 1024), 16, 0, 0);
+    if (nbytes <= kIdxBytes)
+      for (int pc = wave; pc * 1024 < nbytes; pc += kWaves)
+        __builtin_amdgcn_global_load_lds(DOL_GPTR(entb + a0 + pc * 1024 + lane * 16),
+                                         DOL_LPTR(lds + kIdxBase + (k & 1) * kIdxBytes + pc * 1024), 16, 0, 0);
   };
 
   const int row0 = wave * kRW;  // within the group
@@ -127,7 +140,7 @@ __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
     __syncthreads();                                   // ... and every wave's; buffer (k+1)&1 is free
     if (k + 1 < nk) issue(k + 1);
     if constexpr (PROBE == 1) continue;
-    const uint32_t xbase = uint32_t((k & 1) * kBuf) + lane16;  // LDS byte address of my X piece
+    const uint32_t lb = uint32_t((k & 1) * kXBytes) + lane16;  // stage base | my lane's 16 B
     const int32_t* hk = H + int64_t(k) * (kRows + 1);
     const int e0 = hk[0];
     const int sh = e0 & 1;                    // the block starts 8 B into its first 16-B piece
@@ -140,10 +153,10 @@ __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
       for (int r = 0; r < kRW; ++r)
         for (int e = bnd[r]; e < bnd[r + 1]; ++e)
           acc[r] = fmac(acc[r], __int_as_float(ent[2 * int64_t(e) + 1]),
-                        *reinterpret_cast<const f4*>(lds + xbase + ent[2 * int64_t(e)]));
+                        *reinterpret_cast<const f4*>(lds + piece_addr(uint32_t(ent[2 * int64_t(e)]), lb)));
       continue;
     }
-    const uint8_t* ib = lds + (k & 1) * kBuf + kXBytes + 8 * (sh - e0);  // entry e at ib + 8 e
+    const uint8_t* ib = lds + kIdxBase + (k & 1) * kIdxBytes + 8 * (sh - e0);  // entry e at ib + 8 e
     // Rows in groups of four: lane j of the wave holds the group's entry j
     // (LDS byte offset, weight) in two VGPRs; each neighbour's pair reaches
     // the scalar unit by v_readlane (no memory latency inside the row loops).
@@ -157,7 +170,7 @@ __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
           f4 a = acc[4 * g + i];
           for (int e = bnd[4 * g + i]; e < bnd[4 * g + i + 1]; ++e) {
             const I2 q = *reinterpret_cast<const I2*>(ib + 8 * e);
-            a = fmac(a, __int_as_float(q.y), *reinterpret_cast<const f4*>(lds + xbase + q.x));
+            a = fmac(a, __int_as_float(q.y), *reinterpret_cast<const f4*>(lds + piece_addr(uint32_t(q.x), lb)));
           }
           acc[4 * g + i] = a;
         }
@@ -168,7 +181,7 @@ __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
       // entry j of the group: (LDS byte offset, weight); the lane-distributed
       // copy (vo, vw) is only read in the v_readlane variant
       auto ent_at = [&](int j, uint32_t& o, float& w) {
-        if constexpr (BCAST) {
+        if constexpr (MODE == 1) {
           const I2 e = *reinterpret_cast<const I2*>(ib + 8 * (gs + j));
           o = uint32_t(e.x);
           w = __int_as_float(e.y);
@@ -189,10 +202,10 @@ __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
           ent_at(j + 1, o1, w1);
           ent_at(j + 2, o2, w2);
           ent_at(j + 3, o3, w3);
-          const f4 x0 = *reinterpret_cast<const f4*>(lds + xbase + o0);
-          const f4 x1 = *reinterpret_cast<const f4*>(lds + xbase + o1);
-          const f4 x2 = *reinterpret_cast<const f4*>(lds + xbase + o2);
-          const f4 x3 = *reinterpret_cast<const f4*>(lds + xbase + o3);
+          const f4 x0 = *reinterpret_cast<const f4*>(lds + piece_addr(o0, lb));
+          const f4 x1 = *reinterpret_cast<const f4*>(lds + piece_addr(o1, lb));
+          const f4 x2 = *reinterpret_cast<const f4*>(lds + piece_addr(o2, lb));
+          const f4 x3 = *reinterpret_cast<const f4*>(lds + piece_addr(o3, lb));
           a = fmac(a, w0, x0);
           a = fmac(a, w1, x1);
           a = fmac(a, w2, x2);
@@ -203,8 +216,8 @@ __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
           float w0, w1;
           ent_at(j, o0, w0);
           ent_at(j + 1, o1, w1);
-          const f4 x0 = *reinterpret_cast<const f4*>(lds + xbase + o0);
-          const f4 x1 = *reinterpret_cast<const f4*>(lds + xbase + o1);
+          const f4 x0 = *reinterpret_cast<const f4*>(lds + piece_addr(o0, lb));
+          const f4 x1 = *reinterpret_cast<const f4*>(lds + piece_addr(o1, lb));
           a = fmac(a, w0, x0);
           a = fmac(a, w1, x1);
           j += 2;
@@ -213,7 +226,7 @@ __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
           uint32_t o0;
           float w0;
           ent_at(j, o0, w0);
-          a = fmac(a, w0, *reinterpret_cast<const f4*>(lds + xbase + o0));
+          a = fmac(a, w0, *reinterpret_cast<const f4*>(lds + piece_addr(o0, lb)));
         }
         acc[4 * g + i] = a;
       }
@@ -428,10 +441,10 @@ extern "C" int dol_mix_csr_slab_f32(const float* X, int64_t ldx, int32_t x_rows,
     hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(grid)), dim3(kThreads), kLds, s, X, ldx, x_rows, Y, ldy,
                        n_rows, P, ent, hdr, nk, static_cast<int>(n_rg), n_slabs);
   };
-  static const bool readlane = [] { const char* e = getenv("DOL_SLAB_READLANE"); return e && atoi(e) != 0; }();
+  static const int mode = [] { const char* e = getenv("DOL_SLAB_MODE"); return e ? atoi(e) : 0; }();
   if (probe == 1) launch(csr_slab_kernel<1>);
   else if (probe == 2) launch(csr_slab_kernel<2>);
-  else if (readlane) launch(csr_slab_kernel<0, false>);
+  else if (mode == 2) launch(csr_slab_kernel<0, 2>);
   else launch(csr_slab_kernel<0>);
   return dol::check_launch("dol_mix_csr_slab_f32");
 }
