@@ -90,7 +90,9 @@ __device__ __forceinline__ uint32_t piece_addr(uint32_t o, uint32_t lb) { return
 //   dropped (profiles/r02_slab_probe.txt): the wave's entries as one stream in
 //   windows of 4 / 8 across row boundaries, each entry's accumulator chosen by
 //   a uniform switch on a row tag (5.4 ms; needs 8 waves x 16 rows for
-//   registers, and those slow mode 1 to 1.5 ms); index by scalar loads (2.1 ms).
+//   registers, and those slow mode 1 to 1.5 ms); row pairs in lockstep, four
+//   entries per row per step, clamped reads and branch-skipped arithmetic
+//   (1.73 ms); index by scalar loads (2.1 ms).
 template <int PROBE = 0, int MODE = 1>
 __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
     const float* __restrict__ X, int64_t ldx, int x_rows, float* __restrict__ Y, int64_t ldy, int n_rows, int64_t P,
