@@ -54,12 +54,9 @@ constexpr int kWaves = 16;
 constexpr int kThreads = 64 * kWaves;
 constexpr int kXBytes = kChunk * kCols * 4;  // 64 KiB of X per chunk
 constexpr int kIdxBytes = 16 * 1024;          // index block capacity per chunk (2048 entries)
-// LDS: X stage 0 at 0, X stage 1 at 64 KiB (bits 10-15 of both bases clear, so
-// one v_bfi_b32 merges a piece's offset, the stage base and the lane offset),
-// index stages at 128 KiB and 144 KiB: 160 KiB
+// LDS: X stages at 0 and 64 KiB, index stages at 128 KiB and 144 KiB: 160 KiB
 constexpr int kIdxBase = 2 * kXBytes;
 constexpr int kLds = 2 * kXBytes + 2 * kIdxBytes;
-constexpr uint32_t kPieceMask = 0xFC00u;       // bits of an entry's offset word that select the piece (agent)
 constexpr int kRW = 8;                        // rows per wave
 constexpr int kRows = kWaves * kRW;           // rows per row group
 constexpr int kEntPad = 160;                  // ent pad entries (the block DMA may read 1 KiB + 8 B past a block)
@@ -77,9 +74,8 @@ struct I2 {
 // vs 1.33 with the per-component scalar form at 1024 x 101,770, same bits)
 __device__ __forceinline__ f4 fmac(f4 acc, float w, f4 x) { return acc + x * w; }
 
-// LDS byte address of entry word `o`'s piece for this lane (stage base | lane * 16
-// in `lb`): one v_bfi_b32
-__device__ __forceinline__ uint32_t piece_addr(uint32_t o, uint32_t lb) { return (o & kPieceMask) | (lb & ~kPieceMask); }
+// LDS byte address of entry word `o`'s piece for this lane (stage base + lane * 16 in `lb`)
+__device__ __forceinline__ uint32_t piece_addr(uint32_t o, uint32_t lb) { return o + lb; }
 
 // PROBE (diagnostics, DOL_SLAB_PROBE): 1 = staging only (no gathers), 2 = gathers
 // only (no LDS-DMA: sums of whatever LDS holds; results meaningless).
@@ -92,7 +88,12 @@ __device__ __forceinline__ uint32_t piece_addr(uint32_t o, uint32_t lb) { return
 //   a uniform switch on a row tag (5.4 ms; needs 8 waves x 16 rows for
 //   registers, and those slow mode 1 to 1.5 ms); row pairs in lockstep, four
 //   entries per row per step, clamped reads and branch-skipped arithmetic
-//   (1.73 ms); index by scalar loads (2.1 ms).
+//   (1.73 ms); the wave's entries as one stream in steps of up to 4 entries of
+//   one row, the next step's index read across row boundaries, one branch per
+//   step on the slot count (1.35-1.38 ms); index by scalar loads (2.1 ms).
+// Chunk headers (row starts, the next block's bounds) arrive by vector loads
+// issued with the chunk's DMA, so the chunk loop has no scalar-load waits
+// (1.105-1.12 vs 1.135-1.147 ms with s_load headers).
 template <int PROBE = 0, int MODE = 1>
 __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
     const float* __restrict__ X, int64_t ldx, int x_rows, float* __restrict__ Y, int64_t ldy, int n_rows, int64_t P,
@@ -111,6 +112,9 @@ __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
   const int32_t* H = hdr + int64_t(rg) * nk * (kRows + 1);  // this row group's blocks
   const uint8_t* entb = reinterpret_cast<const uint8_t*>(ent);
 
+  const int row0 = wave * kRW;  // within the group
+  int blk0 = H[0], blk1 = H[kRows];  // chunk 0's index block [blk0, blk1)
+  int hv = 0;                         // header lanes, see issue()
   auto issue = [&](int k) {
     if constexpr (PROBE == 2) return;
     uint8_t* dst = lds + (k & 1) * kXBytes;
@@ -121,16 +125,19 @@ __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
       __builtin_amdgcn_global_load_lds(DOL_GPTR(xsrc + int64_t(a) * ldx), DOL_LPTR(dst + al * 1024), 16, 0, 0);
     }
     // the chunk's index block (16-B aligned start, whole 1 KiB pieces; ent is padded)
-    const int64_t e0 = H[int64_t(k) * (kRows + 1)], e1 = H[int64_t(k) * (kRows + 1) + kRows];
-    const int64_t a0 = (e0 * 8) & ~int64_t(15);
-    const int64_t nbytes = e1 * 8 - a0;
+    const int64_t a0 = (int64_t(blk0) * 8) & ~int64_t(15);
+    const int64_t nbytes = int64_t(blk1) * 8 - a0;
     if (nbytes <= kIdxBytes)
       for (int pc = wave; pc * 1024 < nbytes; pc += kWaves)
         __builtin_amdgcn_global_load_lds(DOL_GPTR(entb + a0 + pc * 1024 + lane * 16),
                                          DOL_LPTR(lds + kIdxBase + (k & 1) * kIdxBytes + pc * 1024), 16, 0, 0);
+    // headers ride the same vmcnt wait: lanes 0..kRW hold chunk k's row starts of
+    // this wave's rows, lanes kRW+1 / kRW+2 chunk k+1's block bounds
+    const int hl = lane <= kRW ? row0 + lane : (lane == kRW + 1 ? 0 : kRows);
+    const int kk = lane <= kRW ? k : min(k + 1, nk - 1);
+    if (lane <= kRW + 2) hv = H[int64_t(kk) * (kRows + 1) + hl];
   };
 
-  const int row0 = wave * kRW;  // within the group
   f4 acc[kRW];
 #pragma unroll
   for (int r = 0; r < kRW; ++r) acc[r] = f4{0.f, 0.f, 0.f, 0.f};
@@ -138,18 +145,19 @@ __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
 
   issue(0);
   for (int k = 0; k < nk; ++k) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // my pieces of chunk k landed
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // my pieces (and header lanes) of chunk k landed
     __syncthreads();                                   // ... and every wave's; buffer (k+1)&1 is free
-    if (k + 1 < nk) issue(k + 1);
-    if constexpr (PROBE == 1) continue;
-    const uint32_t lb = uint32_t((k & 1) * kXBytes) + lane16;  // stage base | my lane's 16 B
-    const int32_t* hk = H + int64_t(k) * (kRows + 1);
-    const int e0 = hk[0];
-    const int sh = e0 & 1;                    // the block starts 8 B into its first 16-B piece
-    const bool fits = int64_t(hk[kRows]) * 8 - ((int64_t(e0) * 8) & ~int64_t(15)) <= kIdxBytes;
     int bnd[kRW + 1];
 #pragma unroll
-    for (int i = 0; i <= kRW; ++i) bnd[i] = hk[row0 + i];
+    for (int i = 0; i <= kRW; ++i) bnd[i] = __builtin_amdgcn_readlane(hv, i);
+    const int e0 = blk0;
+    const bool fits = int64_t(blk1) * 8 - ((int64_t(e0) * 8) & ~int64_t(15)) <= kIdxBytes;
+    blk0 = __builtin_amdgcn_readlane(hv, kRW + 1);  // chunk k+1's block, for issue(k + 1)
+    blk1 = __builtin_amdgcn_readlane(hv, kRW + 2);
+    if (k + 1 < nk) issue(k + 1);
+    if constexpr (PROBE == 1) continue;
+    const uint32_t lb = uint32_t((k & 1) * kXBytes) + lane16;  // stage base + my lane's 16 B
+    const int sh = e0 & 1;                    // the block starts 8 B into its first 16-B piece
     if (!fits) {  // an over-full block (denser graphs): indices from global memory, same order
 #pragma unroll
       for (int r = 0; r < kRW; ++r)
