@@ -66,8 +66,8 @@ static_assert(kChunk % kWaves == 0, "chunk must split evenly over the waves");
 #define DOL_GPTR(p) ((const __attribute__((address_space(1))) void*)(p))
 #define DOL_LPTR(p) ((__attribute__((address_space(3))) void*)(p))
 
-struct I2 {
-  int32_t x, y;  // (LDS byte offset of the neighbour's piece in its chunk, weight bits)
+struct alignas(16) I4 {
+  int32_t x, y, z, w;  // two (LDS byte offset of the neighbour's piece in its chunk, weight bits) entries
 };
 
 // separately rounded mul, then add (v_pk_mul_f32 / v_pk_add_f32 pairs: 1.18 ms
@@ -79,22 +79,22 @@ __device__ __forceinline__ uint32_t piece_addr(uint32_t o, uint32_t lb) { return
 
 // PROBE (diagnostics, DOL_SLAB_PROBE): 1 = staging only (no gathers), 2 = gathers
 // only (no LDS-DMA: sums of whatever LDS holds; results meaningless).
-// MODE 1 (default): rows one by one in groups of 4 / 2 / 1 entries, each
-//   group's (offset, weight) pairs by uniform LDS reads (ds_read2_b64) into
-//   VGPRs; MODE 2 (DOL_SLAB_MODE=2): by v_readlane from the group's
-//   lane-distributed index.  1024 x 101,770: 1.12 vs 1.17 ms.  Tried and
-//   dropped (profiles/r02_slab_probe.txt): the wave's entries as one stream in
-//   windows of 4 / 8 across row boundaries, each entry's accumulator chosen by
-//   a uniform switch on a row tag (5.4 ms; needs 8 waves x 16 rows for
-//   registers, and those slow mode 1 to 1.5 ms); row pairs in lockstep, four
-//   entries per row per step, clamped reads and branch-skipped arithmetic
-//   (1.73 ms); the wave's entries as one stream in steps of up to 4 entries of
-//   one row, the next step's index read across row boundaries, one branch per
-//   step on the slot count (1.35-1.38 ms); index by scalar loads (2.1 ms).
-// Chunk headers (row starts, the next block's bounds) arrive by vector loads
-// issued with the chunk's DMA, so the chunk loop has no scalar-load waits
-// (1.105-1.12 vs 1.135-1.147 ms with s_load headers).
-template <int PROBE = 0, int MODE = 1>
+// Each row walks its chunk segment in groups of 4 / 2 / 1 entries: the index
+// pairs by uniform ds_read_b128 (segments are padded to even lengths, so two
+// entries share one 16-B LDS read: 2 LDS cycles per entry; ds_read2_b64 took
+// 4), then the gathers, then separately rounded packed mul / add.
+// Tried and dropped (1024 x 101,770; profiles/r02_slab_probe.txt): index by
+// v_readlane from a lane-distributed group index (1.17 ms vs 1.12 with
+// ds_read2_b64 pairs); the wave's entries as one stream in windows of 4 / 8
+// across row boundaries with the accumulator chosen by a uniform switch on a
+// row tag (5.4 ms; needs 8 waves x 16 rows for registers, which slow the rest
+// to 1.5 ms); row pairs in lockstep, 4 entries per row per step, clamped
+// reads, branch-skipped arithmetic (1.73 ms); one stream in steps of up to 4
+// entries of one row with the next step's index read across rows (1.35 ms);
+// index by scalar loads (2.1 ms).  Chunk headers (row starts, the next block's
+// bounds) arrive by vector loads issued with the chunk's DMA, so the chunk
+// loop has no scalar-load waits (1.105-1.12 vs 1.135-1.147 ms with s_load).
+template <int PROBE = 0>
 __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
     const float* __restrict__ X, int64_t ldx, int x_rows, float* __restrict__ Y, int64_t ldy, int n_rows, int64_t P,
     const int32_t* __restrict__ ent, const int32_t* __restrict__ hdr, int nk, int n_rg, int64_t n_slabs) {
@@ -125,8 +125,8 @@ __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
       __builtin_amdgcn_global_load_lds(DOL_GPTR(xsrc + int64_t(a) * ldx), DOL_LPTR(dst + al * 1024), 16, 0, 0);
     }
     // the chunk's index block (16-B aligned start, whole 1 KiB pieces; ent is padded)
-    const int64_t a0 = (int64_t(blk0) * 8) & ~int64_t(15);
-    const int64_t nbytes = int64_t(blk1) * 8 - a0;
+    const int64_t a0 = int64_t(blk0 & ~1) * 8;  // even: 16-B aligned
+    const int64_t nbytes = int64_t(blk1 & ~1) * 8 - a0;
     if (nbytes <= kIdxBytes)
       for (int pc = wave; pc * 1024 < nbytes; pc += kWaves)
         __builtin_amdgcn_global_load_lds(DOL_GPTR(entb + a0 + pc * 1024 + lane * 16),
@@ -147,99 +147,58 @@ __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
   for (int k = 0; k < nk; ++k) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // my pieces (and header lanes) of chunk k landed
     __syncthreads();                                   // ... and every wave's; buffer (k+1)&1 is free
-    int bnd[kRW + 1];
+    int bnd[kRW + 1];  // header words: (even) first entry | 1 if the row's segment ends in a pad entry
 #pragma unroll
     for (int i = 0; i <= kRW; ++i) bnd[i] = __builtin_amdgcn_readlane(hv, i);
-    const int e0 = blk0;
-    const bool fits = int64_t(blk1) * 8 - ((int64_t(e0) * 8) & ~int64_t(15)) <= kIdxBytes;
+    const int e0 = blk0 & ~1;
+    const bool fits = int64_t((blk1 & ~1) - e0) * 8 <= kIdxBytes;
     blk0 = __builtin_amdgcn_readlane(hv, kRW + 1);  // chunk k+1's block, for issue(k + 1)
     blk1 = __builtin_amdgcn_readlane(hv, kRW + 2);
     if (k + 1 < nk) issue(k + 1);
     if constexpr (PROBE == 1) continue;
     const uint32_t lb = uint32_t((k & 1) * kXBytes) + lane16;  // stage base + my lane's 16 B
-    const int sh = e0 & 1;                    // the block starts 8 B into its first 16-B piece
     if (!fits) {  // an over-full block (denser graphs): indices from global memory, same order
 #pragma unroll
-      for (int r = 0; r < kRW; ++r)
-        for (int e = bnd[r]; e < bnd[r + 1]; ++e)
+      for (int r = 0; r < kRW; ++r) {
+        const int s = bnd[r] & ~1, n = (bnd[r + 1] & ~1) - s - (bnd[r] & 1);
+        for (int e = s; e < s + n; ++e)
           acc[r] = fmac(acc[r], __int_as_float(ent[2 * int64_t(e) + 1]),
                         *reinterpret_cast<const f4*>(lds + piece_addr(uint32_t(ent[2 * int64_t(e)]), lb)));
+      }
       continue;
     }
-    const uint8_t* ib = lds + kIdxBase + (k & 1) * kIdxBytes + 8 * (sh - e0);  // entry e at ib + 8 e
-    // Rows in groups of four: lane j of the wave holds the group's entry j
-    // (LDS byte offset, weight) in two VGPRs; each neighbour's pair reaches
-    // the scalar unit by v_readlane (no memory latency inside the row loops).
+    // the block in LDS as 16-B pairs of entries (every row segment starts on an
+    // even entry, so a pair never straddles two rows' segments): one uniform
+    // ds_read_b128 (4 LDS cycles) carries two (offset, weight) entries
+    const I4* ib4 = reinterpret_cast<const I4*>(lds + kIdxBase + (k & 1) * kIdxBytes);
+    auto gather = [&](uint32_t o) { return *reinterpret_cast<const f4*>(lds + piece_addr(o, lb)); };
 #pragma unroll
-    for (int g = 0; g < kRW / 4; ++g) {
-      const int gs = bnd[4 * g], ge = bnd[4 * g + 4];
-      if (ge == gs) continue;
-      if (ge - gs > 64) {  // a group with more than 64 entries in this chunk: uniform LDS reads
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          f4 a = acc[4 * g + i];
-          for (int e = bnd[4 * g + i]; e < bnd[4 * g + i + 1]; ++e) {
-            const I2 q = *reinterpret_cast<const I2*>(ib + 8 * e);
-            a = fmac(a, __int_as_float(q.y), *reinterpret_cast<const f4*>(lds + piece_addr(uint32_t(q.x), lb)));
-          }
-          acc[4 * g + i] = a;
-        }
-        continue;
+    for (int r = 0; r < kRW; ++r) {
+      const int s = (bnd[r] & ~1) - e0;  // pair-aligned, relative to the block
+      const int n = (bnd[r + 1] & ~1) - (bnd[r] & ~1) - (bnd[r] & 1);
+      f4 a = acc[r];
+      int j = 0;
+      for (; j + 4 <= n; j += 4) {
+        const I4 q0 = ib4[(s + j) >> 1], q1 = ib4[((s + j) >> 1) + 1];
+        const f4 x0 = gather(uint32_t(q0.x)), x1 = gather(uint32_t(q0.z));
+        const f4 x2 = gather(uint32_t(q1.x)), x3 = gather(uint32_t(q1.z));
+        a = fmac(a, __int_as_float(q0.y), x0);
+        a = fmac(a, __int_as_float(q0.w), x1);
+        a = fmac(a, __int_as_float(q1.y), x2);
+        a = fmac(a, __int_as_float(q1.w), x3);
       }
-      const I2 q = *reinterpret_cast<const I2*>(ib + 8 * min(gs + lane, ge - 1));
-      const int vo = q.x, vw = q.y;
-      // entry j of the group: (LDS byte offset, weight); the lane-distributed
-      // copy (vo, vw) is only read in the v_readlane variant
-      auto ent_at = [&](int j, uint32_t& o, float& w) {
-        if constexpr (MODE == 1) {
-          const I2 e = *reinterpret_cast<const I2*>(ib + 8 * (gs + j));
-          o = uint32_t(e.x);
-          w = __int_as_float(e.y);
-        } else {
-          o = uint32_t(__builtin_amdgcn_readlane(vo, j));
-          w = __int_as_float(__builtin_amdgcn_readlane(vw, j));
-        }
-      };
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int j1 = bnd[4 * g + i + 1] - gs;
-        int j = bnd[4 * g + i] - gs;
-        f4 a = acc[4 * g + i];
-        for (; j + 4 <= j1; j += 4) {
-          uint32_t o0, o1, o2, o3;
-          float w0, w1, w2, w3;
-          ent_at(j, o0, w0);
-          ent_at(j + 1, o1, w1);
-          ent_at(j + 2, o2, w2);
-          ent_at(j + 3, o3, w3);
-          const f4 x0 = *reinterpret_cast<const f4*>(lds + piece_addr(o0, lb));
-          const f4 x1 = *reinterpret_cast<const f4*>(lds + piece_addr(o1, lb));
-          const f4 x2 = *reinterpret_cast<const f4*>(lds + piece_addr(o2, lb));
-          const f4 x3 = *reinterpret_cast<const f4*>(lds + piece_addr(o3, lb));
-          a = fmac(a, w0, x0);
-          a = fmac(a, w1, x1);
-          a = fmac(a, w2, x2);
-          a = fmac(a, w3, x3);
-        }
-        if (j + 2 <= j1) {
-          uint32_t o0, o1;
-          float w0, w1;
-          ent_at(j, o0, w0);
-          ent_at(j + 1, o1, w1);
-          const f4 x0 = *reinterpret_cast<const f4*>(lds + piece_addr(o0, lb));
-          const f4 x1 = *reinterpret_cast<const f4*>(lds + piece_addr(o1, lb));
-          a = fmac(a, w0, x0);
-          a = fmac(a, w1, x1);
-          j += 2;
-        }
-        if (j < j1) {
-          uint32_t o0;
-          float w0;
-          ent_at(j, o0, w0);
-          a = fmac(a, w0, *reinterpret_cast<const f4*>(lds + piece_addr(o0, lb)));
-        }
-        acc[4 * g + i] = a;
+      if (j + 2 <= n) {
+        const I4 q0 = ib4[(s + j) >> 1];
+        const f4 x0 = gather(uint32_t(q0.x)), x1 = gather(uint32_t(q0.z));
+        a = fmac(a, __int_as_float(q0.y), x0);
+        a = fmac(a, __int_as_float(q0.w), x1);
+        j += 2;
       }
+      if (j < n) {
+        const I4 q0 = ib4[(s + j) >> 1];
+        a = fmac(a, __int_as_float(q0.y), gather(uint32_t(q0.x)));
+      }
+      acc[r] = a;
     }
   }
   if (p >= P) return;
@@ -366,7 +325,7 @@ __global__ __launch_bounds__(256) void slab_count_kernel(const int32_t* __restri
     const int lo = lower_bound_col(col, e0, e1, k * kChunk);
     c = lower_bound_col(col, lo, e1, (k + 1) * kChunk) - lo;
   }
-  hdr[idx] = c;
+  hdr[idx] = c + (c & 1);  // segments padded to even lengths
 }
 
 // in-place exclusive scan of hdr[0..len) (one workgroup: a contiguous segment per thread)
@@ -394,11 +353,13 @@ __global__ __launch_bounds__(1024) void slab_scan_kernel(int32_t* __restrict__ h
   }
 }
 
-// one wave per row: entries to their chunk-major slots as (LDS byte offset, weight bits)
+// one wave per row: entries to their chunk-major slots as (LDS byte offset,
+// weight bits); then, per chunk with an odd count, a (0, 0) pad entry closes the
+// segment and bit 0 of the segment's header word is set
 __global__ __launch_bounds__(64) void slab_scatter_kernel(const int32_t* __restrict__ rowptr,
                                                           const int32_t* __restrict__ col,
                                                           const float* __restrict__ val, int nk,
-                                                          const int32_t* __restrict__ hdr, int32_t* __restrict__ ent) {
+                                                          int32_t* __restrict__ hdr, int32_t* __restrict__ ent) {
   const int r = blockIdx.x, g = r / kRows, i = r % kRows;
   const int e0 = rowptr[r], e1 = rowptr[r + 1];
   for (int e = e0 + int(threadIdx.x); e < e1; e += 64) {
@@ -407,6 +368,18 @@ __global__ __launch_bounds__(64) void slab_scatter_kernel(const int32_t* __restr
     const int64_t dst = hdr[(int64_t(g) * nk + k) * (kRows + 1) + i] + (e - first);
     ent[2 * dst] = (c % kChunk) * (kCols * 4);
     ent[2 * dst + 1] = __float_as_int(val[e]);
+  }
+  __syncthreads();  // every header read above is done before the pad bits change them
+  for (int k = int(threadIdx.x); k < nk; k += 64) {
+    const int lo = lower_bound_col(col, e0, e1, k * kChunk);
+    const int n = lower_bound_col(col, lo, e1, (k + 1) * kChunk) - lo;
+    if (n & 1) {
+      int32_t* h = hdr + (int64_t(g) * nk + k) * (kRows + 1) + i;
+      const int64_t pad = *h + n;
+      ent[2 * pad] = 0;
+      ent[2 * pad + 1] = 0;
+      *h |= 1;
+    }
   }
 }
 
@@ -419,9 +392,9 @@ extern "C" int64_t dol_csr_slab_hdr_len(int32_t n_rows, int32_t x_rows) {
   if (n_rows <= 0 || x_rows <= 0) return 0;
   return cdiv(n_rows, kRows) * dol_csr_slab_nk(x_rows) * (kRows + 1);
 }
-extern "C" int64_t dol_csr_slab_ent_len(int64_t nnz_cap) {
-  if (nnz_cap < 0 || nnz_cap > dol::kMaxDim) return 0;
-  return 2 * (nnz_cap + kEntPad);
+extern "C" int64_t dol_csr_slab_ent_len(int64_t nnz_cap, int32_t n_rows, int32_t x_rows) {
+  if (nnz_cap < 0 || nnz_cap > dol::kMaxDim || n_rows < 0 || x_rows < 0) return 0;
+  return 2 * (nnz_cap + int64_t(n_rows) * dol_csr_slab_nk(x_rows) + kEntPad);  // + one pad per (row, chunk)
 }
 
 extern "C" int dol_mix_csr_slab_f32(const float* X, int64_t ldx, int32_t x_rows, float* Y, int64_t ldy,
@@ -451,10 +424,8 @@ extern "C" int dol_mix_csr_slab_f32(const float* X, int64_t ldx, int32_t x_rows,
     hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(grid)), dim3(kThreads), kLds, s, X, ldx, x_rows, Y, ldy,
                        n_rows, P, ent, hdr, nk, static_cast<int>(n_rg), n_slabs);
   };
-  static const int mode = [] { const char* e = getenv("DOL_SLAB_MODE"); return e ? atoi(e) : 0; }();
   if (probe == 1) launch(csr_slab_kernel<1>);
   else if (probe == 2) launch(csr_slab_kernel<2>);
-  else if (mode == 2) launch(csr_slab_kernel<0, 2>);
   else launch(csr_slab_kernel<0>);
   return dol::check_launch("dol_mix_csr_slab_f32");
 }

@@ -66,7 +66,7 @@ SIGNATURES = {
     "dol_transpose_f32": [_ptr, _i64, _ptr, _i64, _i64, _i64, _ptr],
     "dol_csr_slab_nk": [_i32],
     "dol_csr_slab_hdr_len": [_i32, _i32],
-    "dol_csr_slab_ent_len": [_i64],
+    "dol_csr_slab_ent_len": [_i64, _i32, _i32],
     "dol_mix_csr_slab_f32": [_ptr, _i64, _i32, _ptr, _i64, _i32, _i64, _ptr, _ptr, _ptr],
     "dol_csr_slab_pack": [_ptr, _ptr, _ptr, _i32, _i32, _ptr, _ptr, _ptr],
     "dol_dense_to_csr_f32": [_ptr, _i64, _i32, _i32, _ptr, _ptr, _ptr, _i64, _ptr],

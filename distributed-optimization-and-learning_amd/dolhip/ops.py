@@ -130,12 +130,14 @@ def csr_slab_pack(rowptr: torch.Tensor, col: torch.Tensor, val: torch.Tensor, x_
                   ent: Optional[torch.Tensor] = None, hdr: Optional[torch.Tensor] = None):
     """(ent, hdr) of a device CSR for mix_csr_slab (dol_csr_slab_pack): the
     entries re-packed chunk-major per group of SLAB_ROWS rows as (LDS byte
-    offset, weight bits) pairs, hdr[g][k][i] = first entry of row g*ROWS+i in
-    chunk k.  col/val may be longer than nnz (a capacity); ent is sized from it."""
+    offset, weight bits) pairs, every (row, chunk) segment padded to an even
+    length; hdr[g][k][i] = first entry of row g*ROWS+i in chunk k, bit 0 = the
+    segment ends in a pad.  col/val may be longer than nnz (a capacity); ent
+    is sized from it."""
     n = rowptr.numel() - 1
     _check_csr(rowptr, col, val, rowptr.device)
     L = _native.lib()
-    need_e = int(L.dol_csr_slab_ent_len(col.numel()))
+    need_e = int(L.dol_csr_slab_ent_len(col.numel(), n, int(x_rows)))
     need_h = int(L.dol_csr_slab_hdr_len(n, int(x_rows)))
     if ent is None or ent.numel() < need_e:
         ent = torch.empty(max(need_e, 4), dtype=torch.int32, device=rowptr.device)

@@ -82,9 +82,12 @@ int dol_mix_csr_pm_f32(const float* XT, int64_t ldx, int32_t x_rows, float* YT, 
  * ascending column order.  The CSR comes re-packed chunk-major by
  * dol_csr_slab_pack (rows in groups of DOL_SLAB_ROWS; for group g and chunk k
  * the entries of the group's rows with columns in the chunk are contiguous):
- *   ent  int32 [dol_csr_slab_ent_len(nnz)]: (LDS byte offset, weight bits) pairs
+ *   ent  int32 [dol_csr_slab_ent_len(nnz, n_rows, x_rows)]: (LDS byte offset,
+ *        weight bits) entries; every (row, chunk) segment padded to an even
+ *        number of entries with a (0, 0) entry
  *   hdr  int32 [dol_csr_slab_hdr_len(n_rows, x_rows)]: hdr[g][k][i] = ent
- *        index of row g*DOL_SLAB_ROWS+i's first entry in chunk k (i <= ROWS)
+ *        index of row g*DOL_SLAB_ROWS+i's first entry in chunk k (i <= ROWS;
+ *        even), bit 0 set when that segment ends in a pad entry
  * Limits: ldx, ldy multiples of 4, ldx >= round_up(P, 4) (X rows readable in
  * whole 16-B pieces), X, Y and ent 16-B aligned, X and Y not aliased.
  */
@@ -92,7 +95,7 @@ int dol_mix_csr_pm_f32(const float* XT, int64_t ldx, int32_t x_rows, float* YT, 
 #define DOL_SLAB_ROWS 128
 int dol_csr_slab_nk(int32_t x_rows);
 int64_t dol_csr_slab_hdr_len(int32_t n_rows, int32_t x_rows);
-int64_t dol_csr_slab_ent_len(int64_t nnz_capacity);
+int64_t dol_csr_slab_ent_len(int64_t nnz_capacity, int32_t n_rows, int32_t x_rows);
 int dol_mix_csr_slab_f32(const float* X, int64_t ldx, int32_t x_rows, float* Y, int64_t ldy, int32_t n_rows,
                          int64_t P, const int32_t* ent, const int32_t* hdr, hipStream_t s);
 /* ent and hdr (above) of a device CSR (rowptr / col / val as dol_mix_csr_f32,

@@ -103,17 +103,18 @@ def test_slab_rectangular_and_low_degree_rows(gpu):
 def slab_pack_host(csr, x_rows):
     """Host restatement of dol_csr_slab_pack: rows in groups of SLAB_ROWS; for
     group g, chunk k the rows' chunk-k entries contiguous in (row, column)
-    order; entry = (LDS byte offset (col % 64) * 1024, weight bits)."""
+    order, each row's segment padded to an even length with a (0, 0) entry;
+    entry = (LDS byte offset (col % 64) * 1024, weight bits); header word =
+    segment start | (1 if padded)."""
     R, C = ops.SLAB_ROWS, ops.SLAB_CHUNK
     nk = -(-x_rows // C)
     n_rg = -(-csr.n_rows // R)
     hdr = np.zeros((n_rg, nk, R + 1), np.int64)
     ent = []
-    pos = 0
     for g in range(n_rg):
         for k in range(nk):
             for i in range(R + 1):
-                hdr[g, k, i] = pos
+                hdr[g, k, i] = len(ent)
                 r = g * R + i
                 if i == R or r >= csr.n_rows:
                     continue
@@ -122,7 +123,9 @@ def slab_pack_host(csr, x_rows):
                 sel = (cols >= k * C) & (cols < (k + 1) * C)
                 for c, v in zip(cols[sel], vals[sel]):
                     ent.append(((int(c) % C) * 1024, int(np.float32(v).view(np.int32))))
-                    pos += 1
+                if sel.sum() % 2:
+                    ent.append((0, 0))
+                    hdr[g, k, i] |= 1
     return hdr, np.array(ent, np.int64).reshape(-1, 2)
 
 
@@ -133,7 +136,7 @@ def test_slab_pack_matches_host(n, p, gpu):
     hdr, ent = slab_pack_host(csr, n)
     got_h = plan.hdr[: hdr.size].cpu().numpy().reshape(hdr.shape)
     assert np.array_equal(got_h, hdr)
-    got_e = plan.ent[: 2 * csr.nnz].cpu().numpy().reshape(-1, 2)
+    got_e = plan.ent[: 2 * len(ent)].cpu().numpy().reshape(-1, 2)
     assert np.array_equal(got_e, ent)
 
 
