@@ -34,6 +34,7 @@
 // not bit-exact.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <math.h>
 #include <type_traits>
 
@@ -141,12 +142,12 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
   }
 }
 
-constexpr int kStages = 3;  // F1 LDS-DMA pipeline depth (two chunks in flight during the MFMAs)
+constexpr int kStages = 3;  // default F1 LDS-DMA pipeline depth (NS - 1 chunks in flight during the MFMAs)
 
 // LDS layout of mlp_fwd_kernel (floats): [ union: F1 staging | Hs, W2s, Zs ] [ b1s, b2s, ls ] [ ys ]
-__host__ __device__ inline int64_t fwd_union_floats(int B, int h, int c) {
+__host__ __device__ inline int64_t fwd_union_floats(int B, int h, int c, int ns = kStages) {
   const int64_t Bp = 32 * ((B + 31) / 32);
-  const int64_t staging = int64_t(kStages) * (h + Bp) * 32;
+  const int64_t staging = int64_t(ns) * (h + Bp) * 32;
   const int64_t post = int64_t(B) * (h + 4) + int64_t(c) * (h + 4) + int64_t(B) * c;
   return staging > post ? staging : post;
 }
@@ -159,7 +160,7 @@ __host__ __device__ inline int64_t fwd_union_floats(int B, int h, int c) {
 // deep; a row-contiguous load touches 8 lines per instruction where reading
 // the MFMA fragments straight from HBM touched 64 (2.3 TB/s effective).
 // NT = accumulator tiles per wave: 1 when h * ceil(B/32) <= 128, else 4.
-template <int NT, int UPD, bool TH, bool AL>
+template <int NT, int UPD, bool TH, bool AL, int NS = kStages>
 __global__ __launch_bounds__(kThreads) void mlp_fwd_kernel(MlpArgs a, float* __restrict__ ws) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int B = a.B, d = a.d, h = a.h, c = a.c;
@@ -167,7 +168,7 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd_kernel(MlpArgs a, float* __r
   float* Hs = lds;                   // [B][hp]  H, later dZ1   (after F1)
   float* W2s = Hs + B * hp;          // [c][hp]                 (after F1)
   float* Zs = W2s + c * hp;          // [B][c]   Z2, later dZ2
-  float* b1s = lds + fwd_union_floats(B, h, c);  // [h]
+  float* b1s = lds + fwd_union_floats(B, h, c, NS);  // [h]
   float* b2s = b1s + h;              // [c]
   float* ls = b2s + c;               // [B] per-sample loss
   int* ys = reinterpret_cast<int*>(ls + B);  // [B]
@@ -209,7 +210,7 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd_kernel(MlpArgs a, float* __r
   const int nk = (d + 31) / 32;
   float* stg = lds;
   auto issue = [&](int kc) {
-    float* st = stg + (kc % kStages) * rows * 32;
+    float* st = stg + (kc % NS) * rows * 32;
     for (int i = 0; i < ipw; ++i) {
       const int ins = wave + kWaves * i;
       const int r = 8 * ins + (lane >> 3);
@@ -226,12 +227,11 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd_kernel(MlpArgs a, float* __r
   for (int u = 0; u < NT; ++u)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[u][r] = 0.f;
-  issue(0);
-  if (nk > 1) issue(1);
+  for (int s0 = 0; s0 < NS - 1 && s0 < nk; ++s0) issue(s0);
   for (int kc = 0; kc < nk; ++kc) {
-    wait_vmcnt(kc + 1 < nk ? ipw : 0);  // chunk kc landed (kc + 1 may still fly)
-    __builtin_amdgcn_s_barrier();       // ... for every wave; and stage (kc + 2) % 3 is free
-    const float* st = stg + (kc % kStages) * rows * 32;
+    wait_vmcnt(min(NS - 2, nk - 1 - kc) * ipw);  // chunk kc landed (the next NS - 2 may still fly)
+    __builtin_amdgcn_s_barrier();                 // ... for every wave; and stage (kc + NS - 1) % NS is free
+    const float* st = stg + (kc % NS) * rows * 32;
     if (kc == nk - 1 && (d & 31)) {     // zero the clamped k >= d pieces of the tail chunk
       for (int i = 0; i < ipw; ++i) {
         const int ins = wave + kWaves * i;
@@ -240,7 +240,7 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd_kernel(MlpArgs a, float* __r
       }
       __syncthreads();
     }
-    if (kc + 2 < nk) issue(kc + 2);
+    if (kc + NS - 1 < nk) issue(kc + NS - 1);
 #pragma unroll
     for (int u = 0; u < NT; ++u) {
       const int tile = wave + kWaves * u;
@@ -509,6 +509,8 @@ extern "C" int dol_mlp_step_f32(float* w, int64_t ldw, float* grad, int64_t ldg,
   const size_t lds = static_cast<size_t>(dol_mlp_step_lds_bytes(B, h, c));
   if (lds > 160 * 1024) return fail(DOL_EINVAL, "dol_mlp_step_f32: %zu B of LDS per agent exceeds 160 KiB", lds);
   const dim3 grid(static_cast<unsigned>(n_agents)), block(kThreads);
+  // F1 pipeline depth (DOL_MLP_STAGES = 2 / 3 / 4; diagnostics, default 3)
+  static const int stages = [] { const char* e = getenv("DOL_MLP_STAGES"); return e ? atoi(e) : kStages; }();
   const int upd = update ? mode + 1 : 0;
   float* ws = static_cast<float*>(work);
   const int64_t n_blk2 = int64_t((d + 31) / 32) * n_agents;
@@ -517,14 +519,26 @@ extern "C" int dol_mlp_step_f32(float* w, int64_t ldw, float* grad, int64_t ldg,
   auto go = [&](auto ks, auto upd_c, auto th, auto al) {
     constexpr int KS = decltype(ks)::value, U = decltype(upd_c)::value;
     constexpr bool TH = decltype(th)::value, AL = decltype(al)::value;
-    auto fwd = [&](auto kern) {
-      if (lds > 65536)  // above the default dynamic-LDS cap (gfx950 has 160 KiB per CU)
+    auto fwd = [&](auto kern, size_t lds_ns) {
+      if (lds_ns > 65536)  // above the default dynamic-LDS cap (gfx950 has 160 KiB per CU)
         (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  static_cast<int>(lds));
-      hipLaunchKernelGGL(kern, grid, block, lds, s, a, ws);
+                                  static_cast<int>(lds_ns));
+      hipLaunchKernelGGL(kern, grid, block, lds_ns, s, a, ws);
     };
-    if (h * ((B + 31) / 32) <= 128) fwd(mlp_fwd_kernel<1, U, TH, AL>);
-    else fwd(mlp_fwd_kernel<4, U, TH, AL>);
+    auto lds_for = [&](int ns) {
+      return sizeof(float) * (fwd_union_floats(B, h, c, ns) + h + c + B) + sizeof(int) * size_t(B);
+    };
+    const bool nt1 = h * ((B + 31) / 32) <= 128;
+    if (stages == 2) {
+      if (nt1) fwd(mlp_fwd_kernel<1, U, TH, AL, 2>, lds_for(2));
+      else fwd(mlp_fwd_kernel<4, U, TH, AL, 2>, lds_for(2));
+    } else if (stages == 4 && lds_for(4) <= 160 * 1024) {
+      if (nt1) fwd(mlp_fwd_kernel<1, U, TH, AL, 4>, lds_for(4));
+      else fwd(mlp_fwd_kernel<4, U, TH, AL, 4>, lds_for(4));
+    } else {
+      if (nt1) fwd(mlp_fwd_kernel<1, U, TH, AL>, lds);
+      else fwd(mlp_fwd_kernel<4, U, TH, AL>, lds);
+    }
     hipLaunchKernelGGL((mlp_dw1_kernel<KS, U, TH, AL>), grid2, block, 0, s, a, ws);
   };
   auto by_upd = [&](auto ks, auto th, auto al) {
