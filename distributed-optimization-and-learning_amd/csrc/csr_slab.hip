@@ -335,7 +335,15 @@ __global__ __launch_bounds__(1024) void slab_scan_kernel(int32_t* __restrict__ h
   const int64_t seg = (len + 1023) / 1024;
   const int64_t b0 = min(len, int64_t(t) * seg), b1 = min(len, b0 + seg);
   int s = 0;
-  for (int64_t j = b0; j < b1; ++j) s += hdr[j];
+  int64_t j = b0;
+  for (; j + 8 <= b1; j += 8) {  // eight independent loads per round trip
+    int v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = hdr[j + u];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += v[u];
+  }
+  for (; j < b1; ++j) s += hdr[j];
   int v = s;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -346,7 +354,18 @@ __global__ __launch_bounds__(1024) void slab_scan_kernel(int32_t* __restrict__ h
   __syncthreads();
   int off = v - s;
   for (int q = 0; q < w; ++q) off += wsum[q];
-  for (int64_t j = b0; j < b1; ++j) {
+  j = b0;
+  for (; j + 8 <= b1; j += 8) {
+    int v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = hdr[j + u];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      hdr[j + u] = off;
+      off += v[u];
+    }
+  }
+  for (; j < b1; ++j) {
     const int c = hdr[j];
     hdr[j] = off;
     off += c;
