@@ -312,6 +312,12 @@ __global__ __launch_bounds__(kThreads) void ring_mix_dma_kernel(
 // intermediate uses the single-round formula (fl(fl(+0 + wp*a) + wn*b)), so the
 // result is bit-identical to STEPS launches of ring_mix_kernel.  Wrap-around
 // ring inside X (one shard).
+// Tried (profiles/r02_ring_steps_eps_experiments.txt): intermediate levels as
+// fma(wp, a, +0) + wn*b (three packed ops instead of four; exact up to -0 for
+// +0 on the intermediate levels, the last level kept as axpy0 restores the bits)
+// cut the pk ops per thread and tile 1,040 -> 824 but ran 12.63-12.74 vs
+// 12.14-12.16 ms at eps = 5, three A/B pairs on one box: the pass is not
+// VALU-issue bound.
 // ----------------------------------------------------------------------------
 template <int STEPS, int R, typename V = f4>
 __global__ __launch_bounds__(kThreads) void ring_steps_kernel(

@@ -602,6 +602,36 @@ def test_ring_steps_bit_identical_to_single_rounds(steps, n, P, gpu):
     assert bits_equal(Y.cpu().numpy(), want)
 
 
+@pytest.mark.parametrize("steps", [2, 5, 8])
+def test_ring_steps_signed_zeros_and_underflow(steps, gpu):
+    """The fused pass's intermediate levels use fma(wp, a, +0) + wn*b, which may
+    hold -0 where single rounds hold +0; the last level must still match the
+    single rounds bit for bit.  Inputs full of +-0, denormals and values whose
+    products with the (partly negative, partly tiny) weights underflow."""
+    n, P = 97, 1024
+    rng = np.random.default_rng(steps)
+    X = rng.standard_normal((n, P)).astype(np.float32)
+    pick = rng.random((n, P))
+    X[pick < 0.25] = 0.0
+    X[(pick >= 0.25) & (pick < 0.5)] = -0.0
+    X[(pick >= 0.5) & (pick < 0.6)] = np.float32(1e-42) * np.sign(rng.standard_normal(int(((pick >= 0.5) & (pick < 0.6)).sum())))
+    X[(pick >= 0.6) & (pick < 0.65)] = np.float32(1e-30)
+    X[0, :4] = [np.inf, -np.inf, np.nan, 3e38]
+    wp = rng.random(n).astype(np.float32)
+    wn = rng.random(n).astype(np.float32)
+    wp[::3] *= -1
+    wn[1::4] = np.float32(1e-20)
+    wp[2::5] = 0.0
+    want = X
+    for _ in range(steps):
+        want = oracle.mix_ring(want, wp, wn)
+    assert np.signbit(want[want == 0]).sum() == 0, "single rounds never produce -0"
+    Y = torch.empty(n, P, device=gpu)
+    ops.mix_ring_steps(dev(X, gpu), Y, dev(wp, gpu), dev(wn, gpu), steps)
+    torch.cuda.synchronize()
+    assert bits_equal(Y.cpu().numpy(), want)
+
+
 def test_bank_mix_fused_equals_unfused(gpu):
     from dolhip.bank import AgentBank
     torch.manual_seed(5)
