@@ -47,6 +47,7 @@ namespace {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef float f4v __attribute__((ext_vector_type(4)));
 
 constexpr int kTile = 256;                            // BM = BN
 constexpr int kRec = 48;                              // bytes per (row, k-group): 3 pieces x 8 bf16
@@ -120,6 +121,8 @@ __global__ __launch_bounds__(256) void split3_rows_kernel(const float* __restric
 }
 
 // X [K][P] (row stride ldx) -> XB[kg][Pp][48 B]; one thread per (p, kg), p fastest
+// (the r01 pass, DOL_SPLIT3_XPASS1=1; split3_cols4_kernel below is the default:
+// 196 vs 224 us at 1024 x 101,770, profiles/r02_split3_xpass.txt)
 __global__ __launch_bounds__(256) void split3_cols_kernel(const float* __restrict__ X, int64_t ldx, int K, int64_t P,
                                                           int64_t Pp, int Kg, uint8_t* __restrict__ out) {
   const int64_t idx = int64_t(blockIdx.x) * 256 + threadIdx.x;
@@ -133,6 +136,55 @@ __global__ __launch_bounds__(256) void split3_cols_kernel(const float* __restric
     v[j] = (p < P && k < K) ? X[int64_t(k) * ldx + p] : 0.f;
   }
   write_record(v, out + idx * kRec);
+}
+
+// The same records, one thread per (4 columns, kg): eight 16-B row loads and
+// four whole records.  Thread idx's records are bytes [192 idx, 192 idx + 192)
+// of XB (idx = kg Pp/4 + p/4), so a wave's output is 12 KiB contiguous: the
+// records go through LDS (208-B thread pitch against bank conflicts) and leave
+// as twelve fully coalesced 1-KiB stores per wave.  VEC: X rows 16-B aligned
+// (ldx % 4 == 0); the last, partial column group and unaligned X read per
+// element.
+constexpr int kX4Pitch = 208;
+template <bool VEC>
+__global__ __launch_bounds__(256) void split3_cols4_kernel(const float* __restrict__ X, int64_t ldx, int K, int64_t P,
+                                                           int64_t Pp, int Kg, uint8_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t st[256 * kX4Pitch];
+  const int64_t idx = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  const int64_t nq = Pp / 4, total = nq * Kg;
+  if (idx < total) {
+    const int64_t p0 = 4 * (idx % nq);
+    const int kg = int(idx / nq);
+    float v[4][8];
+    const bool whole = VEC && p0 + 4 <= P;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 8 * kg + j;
+      const float* row = X + int64_t(k < K ? k : 0) * ldx + p0;
+      if (whole) {
+        const f4v q = k < K ? *reinterpret_cast<const f4v*>(row) : f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v[c][j] = q[c];
+      } else {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v[c][j] = (k < K && p0 + c < P) ? row[c] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) write_record(v[c], st + threadIdx.x * kX4Pitch + c * kRec);
+  }
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t wbase = (int64_t(blockIdx.x) * 256 + wave * 64) * (4 * kRec);  // first output byte of the wave
+  const int64_t end = total * (4 * kRec);
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    const int o = 1024 * i + 16 * lane;  // byte within the wave's 12 KiB
+    const int t = o / (4 * kRec), w = o - t * (4 * kRec);
+    if (wbase + o < end)
+      *reinterpret_cast<u32x4*>(out + wbase + o) =
+          *reinterpret_cast<const u32x4*>(st + (wave * 64 + t) * kX4Pitch + w);
+  }
 }
 
 // wait until at most N of this wave's vector-memory operations are in flight
@@ -443,8 +495,17 @@ extern "C" int dol_mix_dense_split3_f32(const float* W, int64_t ldw, const float
   if (!fx) {
     const int64_t n = g.Pp * g.Kg;
     if (cdiv(n, 256) >= (int64_t(1) << 32)) return fail(DOL_EINVAL, "dol_mix_dense_split3_f32: X too large");
-    hipLaunchKernelGGL(split3_cols_kernel, dim3(static_cast<unsigned>(cdiv(n, 256))), dim3(256), 0, s, X, ldx, K, P,
-                       g.Pp, static_cast<int>(g.Kg), xb);
+    static const bool per_column = getenv("DOL_SPLIT3_XPASS1") != nullptr;  // diagnostic: the r01 pass
+    const bool vec = reinterpret_cast<uintptr_t>(X) % 16 == 0 && ldx % 4 == 0;
+    if (per_column)
+      hipLaunchKernelGGL(split3_cols_kernel, dim3(static_cast<unsigned>(cdiv(n, 256))), dim3(256), 0, s, X, ldx, K, P,
+                         g.Pp, static_cast<int>(g.Kg), xb);
+    else if (vec)
+      hipLaunchKernelGGL(split3_cols4_kernel<true>, dim3(static_cast<unsigned>(cdiv(n / 4, 256))), dim3(256), 0, s, X,
+                         ldx, K, P, g.Pp, static_cast<int>(g.Kg), xb);
+    else
+      hipLaunchKernelGGL(split3_cols4_kernel<false>, dim3(static_cast<unsigned>(cdiv(n / 4, 256))), dim3(256), 0, s, X,
+                         ldx, K, P, g.Pp, static_cast<int>(g.Kg), xb);
   }
   // diagnostics knobs (tools/gpu_dense_probe.sh); read once per process
   static const int probe = [] { const char* e = getenv("DOL_SPLIT3_PROBE"); return e ? atoi(e) : 0; }();
