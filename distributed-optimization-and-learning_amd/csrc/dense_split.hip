@@ -562,6 +562,7 @@ extern "C" int dol_mix_dense_split3_f32(const float* W, int64_t ldw, const float
     else if (waves8 && probe == 0) launch(dense_split3_kernel<0, false, 2, 4>, kLds, grid, 0, t_main, 512);
     else if (waves8 && probe == 5) launch(dense_split3_kernel<1, false, 2, 4>, kLds, grid, 0, t_main, 512);
     else if (waves8 && probe == 6) launch(dense_split3_kernel<2, false, 2, 4>, kLds, grid, 0, t_main, 512);
+    else if (waves8 && probe == 7) launch(dense_split3_kernel<4, false, 2, 4>, kLds, grid, 0, t_main, 512);
     else launch(dense_split3_kernel<0, false>, kLds, grid, 0, t_main);
   }
   if (narrow_tail && nb_tail == 1)
