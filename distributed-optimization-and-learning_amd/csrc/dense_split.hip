@@ -244,7 +244,8 @@ __device__ __forceinline__ void split8(const float (&v)[8], bf16x8& p0, bf16x8& 
 
 // PROBE (tools only, DOL_SPLIT3_PROBE): 1 = no operand staging (MFMA ceiling of
 // the loop), 2 = staging only (no fragment reads / MFMAs), 3 = as 1 without
-// the output stores, 4 = full kernel without the output stores.  Measured at 8192 x
+// the output stores, 4 = full kernel without the output stores (5 / 6 / 7: 1 / 2 /
+// 4 on the 8-wave tiles).  Measured at 8192 x
 // 101770 (profiles/r01c_dense_split3_probe.txt): full 53 ms, MFMA-only 45 ms,
 // staging-only 20 ms.  Tried and dropped (same box, no gain): fragments
 // double-buffered in registers with the DMA three stages ahead; the
