@@ -22,6 +22,13 @@
 // the second kernel at full occupancy; a single-kernel version that walked
 // each agent's 25 W1 tiles inside the per-agent workgroup ran 2.4x slower
 // (one HBM round trip per tile, 2-3 waves per SIMD; tools/mlp_phase.hip).
+// Phases at 1024 agents (tools/mlp_phase.hip, r02): the forward runs as two
+// lock-stepped waves of 512 workgroups (two per CU by LDS), each ~90 us:
+// staging + F1 56-71 us (4.6 TB/s), F2 + CE 5-6, B2 15-16, HBM idle in the
+// last two.  Tried (r02): agent pieces with the forwards on a side stream and
+// each piece's dW1 on the caller's stream after its forward, so dW1(q)
+// overlaps forward(q + 1): local step 0.496-0.500 ms (2 pieces) / 0.510-0.518
+// (4) vs 0.492-0.493 unsplit, same box (profiles/r02_mlp_split.txt): dropped.
 //   update (every parameter, as dol_prox_admm_sgd_f32):
 //       g' = g [+ (alpha +) rho*(w - theta)];  buf = mom*buf + g' (buf = g' on the
 //       first step);  w = fma(-lr, buf, w)
