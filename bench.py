@@ -16,6 +16,10 @@ Rank 0 prints ONE JSON line.  `roofline` prices the dominant kernel (the
 ring mix) from HIP events around every launch in the timed region;
 `cpu_baseline` times the reference-structured torch-CPU round
 (oracle/ref_cpu.py) on this host on a bounded sample (N=1 only).
+Secondaries (N=1, skipped with --no-primal-dual): FedADMM round (config 4),
+FedLCon eps = 5 fused pass, random 4-regular mix on the parameter-major bank,
+the Erdos-Renyi mix on the matrix cores (split3) and bit-exact, and a whole
+config-5 round (ER draw + device Neighbors + fused MLP local step + exact mix).
 """
 from __future__ import annotations
 
@@ -332,6 +336,64 @@ def er_exact_mix_round(device, N: int = 1024, P: int = 101770, reps: int = 10):
                     "W draw + device Neighbors + packing included in ms_per_round"}
 
 
+def config5_round(device, N: int = 1024, reps: int = 10):
+    """Secondary (BASELINE config 5, N = 1): one whole round of the
+    time-varying-graph MLP workload -- a new Erdos-Renyi p = 0.1 W drawn on the
+    device, the device Neighbors selection + slab packing, one fused local step
+    of every agent's 784-128-10 MLP (dol_mlp_step_f32: forward, CE, backward,
+    momentum SGD; synthetic batch of 32 per agent) and the bit-exact mix of the
+    parameter rows (dol_mix_csr_slab_f32).  Phases timed with events on the
+    launch stream; ms_per_round by the host clock over `reps` rounds."""
+    from dolhip import graph as G
+    from dolhip.bank import AgentBank
+    from dolhip.mlp import BatchedMLP, mlp_layout
+    d, h, c, B = 784, 128, 10, 32
+    bank = AgentBank(N, mlp_layout(d, h, c), device)
+    mlp = BatchedMLP(bank, d, h, c)
+    gen = torch.Generator(device=device).manual_seed(2028)
+    bank.buffer("x").normal_(0, 0.05, generator=gen)
+    bank.buffer("y").zero_()
+    bank.buffer("mom", zero=True)
+    X = torch.empty(N, B, d, device=device).normal_(generator=gen)
+    y = torch.randint(0, c, (N, B), device=device, generator=gen)
+    Wbuf = torch.empty(N, N, device=device)
+    st = {"plan": None, "r": 0}
+    ev = {k: [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+          for k in ("graph", "local", "mix")}
+
+    def one(k=None):
+        rec = (lambda nm, i: ev[nm][k][i].record()) if k is not None else (lambda nm, i: None)
+        st["r"] += 1
+        rec("graph", 0)
+        W = G.erdos_renyi_stochastic_hip(N, 0.1, 2028 * 1000003 + st["r"], device, out=Wbuf)
+        st["plan"] = G.MixingPlan.from_dense(W, dense_kernel="csr", reuse=st["plan"])
+        rec("graph", 1)
+        rec("local", 0)
+        mlp.step(X, y, lr=0.05, momentum=0.5, first_step=False)
+        rec("local", 1)
+        rec("mix", 0)
+        bank.mix(st["plan"])
+        rec("mix", 1)
+    for _ in range(2):
+        one()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for k in range(reps):
+        one(k)
+    torch.cuda.synchronize(device)
+    el = (time.perf_counter() - t0) / reps
+    ms = {k: sum(a.elapsed_time(b) for a, b in v) / reps for k, v in ev.items()}
+    P = bank.P
+    out = {"agents": N, "params": P, "batch": B, "mlp": f"{d}-{h}-{c}", "ms_per_round": el * 1e3,
+           "rounds_per_s": 1.0 / el, "phase_ms": ms,
+           "local_GBps": N * (4 * P + B * d) * 4 / (ms["local"] / 1e3) / 1e9,
+           "what": "config 5 round: ER p=0.1 W drawn on device + device Neighbors/packing, fused MLP local step "
+                   "(momentum SGD) on fp32 MFMA, bit-exact LDS-gather CSR mix of the parameter rows"}
+    del bank, mlp, X, y, Wbuf, st
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -440,6 +502,10 @@ def main():
         dense = dense_mix_round(device)
         exact = er_exact_mix_round(device)
     _log("dense ER done")
+    cfg5 = None
+    if world == 1 and not args.no_primal_dual:
+        cfg5 = config5_round(device)
+    _log("config 5 round done")
 
     traffic = None
     traffic_src = None
@@ -504,6 +570,7 @@ def main():
             "random_regular_pm": rr_pm,
             "dense_er_mix": dense,
             "er_exact_mix": exact,
+            "config5_round": cfg5,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

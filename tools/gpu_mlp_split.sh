@@ -1,3 +1,4 @@
+# (the DOL_MLP_SPLIT code this script drove was removed after the measurement: profiles/r02_mlp_split.txt)
 # config-5 fused MLP step: agent pieces over two streams (DOL_MLP_SPLIT = 1 / 2 / 4), round and local-step times
 set -e
 R=$GRAFT_REPO_ROOT
