@@ -29,6 +29,9 @@
 // each piece's dW1 on the caller's stream after its forward, so dW1(q)
 // overlaps forward(q + 1): local step 0.496-0.500 ms (2 pieces) / 0.510-0.518
 // (4) vs 0.492-0.493 unsplit, same box (profiles/r02_mlp_split.txt): dropped.
+// Also tried: F1 in 16-wide k chunks (64-B rows) with 4 / 6 stages, 40 / 60 KiB
+// of LDS, so all 1024 workgroups are resident at once: 0.515 / 0.522-0.524 vs
+// 0.505 ms (profiles/r02_mlp_split.txt): dropped.
 //   update (every parameter, as dol_prox_admm_sgd_f32):
 //       g' = g [+ (alpha +) rho*(w - theta)];  buf = mom*buf + g' (buf = g' on the
 //       first step);  w = fma(-lr, buf, w)
