@@ -32,6 +32,10 @@
 // Also tried: F1 in 16-wide k chunks (64-B rows) with 4 / 6 stages, 40 / 60 KiB
 // of LDS, so all 1024 workgroups are resident at once: 0.515 / 0.522-0.524 vs
 // 0.505 ms (profiles/r02_mlp_split.txt): dropped.
+// dW1 as the transposed product (operands swapped, so a lane holds 4
+// consecutive W1 columns and W1 / momentum move as 16-B buffer ops, 4 + 4
+// per lane and tile instead of 16 + 16): 0.577-0.579 vs 0.505 ms; each 16-B
+// instruction then touches 32 W1 rows' lines instead of 2 (same profile): dropped.
 //   update (every parameter, as dol_prox_admm_sgd_f32):
 //       g' = g [+ (alpha +) rho*(w - theta)];  buf = mom*buf + g' (buf = g' on the
 //       first step);  w = fma(-lr, buf, w)
