@@ -196,6 +196,15 @@ class ColumnSharded:
             self.x = torch.empty(self.N, self.ld, dtype=torch.float32, device=self.device)
             self.y = torch.empty_like(self.x)
 
+    def set_plan(self, plan) -> None:
+        """A new W for the next rounds (time-varying graphs, BASELINE config 5:
+        every rank draws the same W from the round's seed); same agent count."""
+        if (plan.n_rows, plan.n_cols) != (self.N, self.plan.n_cols):
+            raise ValueError("set_plan: the new W must have the same shape")
+        self.plan = plan
+        self._apply = plan.apply
+        self._apply_dgd = plan.apply_dgd
+
     def local_cols(self, full: torch.Tensor) -> torch.Tensor:
         """This rank's column block of a full [N, >=P] matrix."""
         return full[:, self.c0:self.c1]

@@ -231,3 +231,22 @@ def test_sharded_dgd_ring_matches_single_process(world, N):
         X, M = oracle.dgd_local(oracle.mix_ring(X, wp, wn), T, M, "least_squares", 2, 0.1, 0.5, k == 0)
     assert oracle.bits_equal(np.concatenate([r[1] for r in res]), X)
     assert oracle.bits_equal(np.concatenate([r[2] for r in res]), M)
+
+
+def test_column_sharded_set_plan_swaps_the_mix():
+    """Time-varying W (config 5): set_plan installs the new plan's kernels and
+    refuses a W of another shape; one process, CPU stand-in plans."""
+    from types import SimpleNamespace
+    calls = []
+
+    def plan_of(tag, n=6, m=6):
+        return SimpleNamespace(n_rows=n, n_cols=m, apply=lambda x, y, P=None: calls.append(tag),
+                               apply_dgd=lambda *a, **k: calls.append(tag + "-dgd"))
+    sh = parallel.ColumnSharded(plan_of("a"), 10, "cpu")
+    sh.step()
+    sh.set_plan(plan_of("b"))
+    sh.step()
+    sh.dgd_step(torch.zeros(6, sh.ld))
+    assert calls == ["a", "b", "b-dgd"]
+    with pytest.raises(ValueError):
+        sh.set_plan(plan_of("c", n=7, m=7))

@@ -183,6 +183,57 @@ def test_column_sharded_dense_split3_on_one_gpu(world, N, P, gpu):
     assert oracle.bits_equal(res[0], Y.cpu().numpy())
 
 
+def _exact_column_worker(rank, world, port, N, P, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "distributed-optimization-and-learning_amd"))
+    from dolhip import graph as G, parallel
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = torch.device("cuda:0")
+        plan = None
+        X = np.random.default_rng(23).standard_normal((N, P)).astype(np.float32)
+        sh = parallel.ColumnSharded(G.MixingPlan.from_dense(G.erdos_renyi_stochastic_hip(N, 0.1, 500, dev), "csr"),
+                                    P, dev)
+        sh.x[:, :sh.Pl] = torch.from_numpy(X[:, sh.c0:sh.c1]).to(dev)
+        for r in range(2):  # a new W every round (config 5), every rank draws the same one
+            plan = G.MixingPlan.from_dense(G.erdos_renyi_stochastic_hip(N, 0.1, 500 + r, dev), "csr", reuse=plan)
+            sh.set_plan(plan)
+            sh.step()
+        full = sh.gather(0)
+        torch.cuda.synchronize()
+        q.put((rank, None if full is None else full.cpu().numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,N,P", [(2, 300, 2048 + 64), (3, 130, 1001)])
+def test_column_sharded_exact_er_mix_on_one_gpu(world, N, P, gpu):
+    """Config 5's exact mix (device Neighbors + LDS-gather CSR) over a
+    parameter-column split, two rounds with a new W each: the gathered result
+    is bit-identical to the oracle's consensus (DIST/clients.py:61-69) on the
+    same two draws, whatever the column blocks."""
+    import oracle
+    from dolhip import graph as G
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_exact_column_worker, args=(r, world, port, N, P, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    X = np.random.default_rng(23).standard_normal((N, P)).astype(np.float32)
+    for r in range(2):
+        csr = G.csr_from_dense(G.erdos_renyi_stochastic_hip(N, 0.1, 500 + r, gpu).cpu())
+        X = oracle.mix_csr(X, csr.rowptr, csr.col, csr.val)
+    assert oracle.bits_equal(res[0], X)
+
+
 def _dgd_ring_worker(rank, world, port, N, P, rounds, q):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
