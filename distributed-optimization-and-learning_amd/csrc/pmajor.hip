@@ -397,7 +397,7 @@ int mix_csr_pm_impl(const char* nm, const float* XT, int64_t ldx, int32_t x_rows
   }
   // geometry: 1024-thread workgroups, one per CU.  Up to 4096 agents (one quad
   // per thread): 64 KiB stages, 2 buffers; beyond (two quads per thread, a
-  // p-row up to 32 KiB): 32 KiB stages, 4 buffers.  Measured at 1024 x 2^20
+  // p-row up to 32 KiB): 32 KiB stages, 5 buffers (r02; 4 in r01).  Measured at 1024 x 2^20
   // (one box): 64 KiB x 2 1.511 ms, 32 KiB x 4 1.533, 48 KiB x 3 1.541;
   // 256- / 512-thread workgroups (8 / 16 KiB stages, 2-4 per CU) 1.82 / 1.64;
   // one stage per short-lived workgroup 4.4; a per-wave ring (no workgroup
@@ -462,7 +462,12 @@ int mix_csr_pm_impl(const char* nm, const float* XT, int64_t ldx, int32_t x_rows
     else if (var == 4) go(csr_pm_kernel<kT1, SFc, NBc, Qc, 2, 2, true>);
     else go(csr_pm_kernel<kT1, SFc, NBc, Qc, 2, 2>);
   };
-  if (big) pick(integral_constant<int, 8192>{}, integral_constant<int, 4>{}, integral_constant<int, 2>{});
+  // beyond 4096 agents: five 32-KiB buffers (all 160 KiB, four p-rows in flight):
+  // 10.57-10.59 vs 10.74-10.81 ms (one box), 10.67 vs 11.03 in bench.py (another)
+  // at 8192 x 2^20 (profiles/r02_pm_nbuf.txt); DOL_PM_BIG_NB=4 keeps four
+  static const int big_nb = env_int("DOL_PM_BIG_NB", 5);
+  if (big && big_nb == 5) pick(integral_constant<int, 8192>{}, integral_constant<int, 5>{}, integral_constant<int, 2>{});
+  else if (big) pick(integral_constant<int, 8192>{}, integral_constant<int, 4>{}, integral_constant<int, 2>{});
   else pick(integral_constant<int, 16384>{}, integral_constant<int, 2>{}, integral_constant<int, 1>{});
   return check_launch(nm);
 }
