@@ -66,6 +66,16 @@ def test_pm_mix_random_regular_vs_oracle(n, P, gpu):
     assert bits_equal(run_pm(X, c, gpu, extra=4 * (n % 3)), oracle.mix_csr(X, c.rowptr, c.col, c.val))
 
 
+@pytest.mark.parametrize("n,P", [(1024, 4099), (4097, 3000), (8192, 4096)])
+def test_pm_mix_many_stages_per_workgroup(n, P, gpu):
+    """Enough p-rows that every persistent workgroup cycles through its whole
+    LDS-DMA ring many times (beyond 4096 agents: five 32-KiB buffers, one p-row
+    each), bit-exact vs the oracle."""
+    c = G.random_regular_csr(n, 4, seed=n + 11)
+    X = np.random.default_rng(n + P).standard_normal((n, P)).astype(np.float32)
+    assert bits_equal(run_pm(X, c, gpu), oracle.mix_csr(X, c.rowptr, c.col, c.val))
+
+
 @pytest.mark.parametrize("nseg", ["1", "3", "8"])
 def test_pm_mix_stage_orders_bit_identical(nseg, gpu, monkeypatch):
     """The stage order (DOL_PM_NSEG segments walked side by side) is a speed
