@@ -408,12 +408,12 @@ int mix_csr_pm_impl(const char* nm, const float* XT, int64_t ldx, int32_t x_rows
   // 64 KiB x 2 and 3.49 with 48 KiB x 3; logistic, no momentum, 2.25 vs 2.43 /
   // 2.55).  DOL_PM_DGD_GEOM (0 / 1 / 2) overrides, for measurement.
   const int dgeo = obj >= 0 ? env_int("DOL_PM_DGD_GEOM", ne == 2 ? 2 : 0) : 0;
-  const bool small5 = !big && obj < 0 && env_int("DOL_PM_SMALL_NB5", 0);  // measurement: 5 x 32 KiB at <= 4096 agents
-  const int SF = big || small5 ? 8192 : (dgeo == 1 ? 12288 : dgeo == 2 ? 20480 : 16384);
+  const int SF = big ? 8192 : (dgeo == 1 ? 12288 : dgeo == 2 ? 20480 : 16384);
   // beyond 4096 agents: five 32-KiB buffers (all 160 KiB, four p-rows in flight)
-  // (profiles/r02_pm_nbuf.txt); DOL_PM_BIG_NB=4 keeps four
+  // (profiles/r02_pm_nbuf.txt); DOL_PM_BIG_NB=4 keeps four.  At <= 4096 agents
+  // 5 x 32 KiB ran level with 2 x 64 KiB (1.56-1.59 ms at 1024 x 2^20)
   static const int big_nb = env_int("DOL_PM_BIG_NB", 5) == 4 ? 4 : 5;
-  const int NB = big ? big_nb : small5 ? 5 : (dgeo == 1 ? 3 : 2);  // must match the kernel's NBUF (LDS size)
+  const int NB = big ? big_nb : (dgeo == 1 ? 3 : 2);  // must match the kernel's NBUF (LDS size)
   int sr = SF / (xw + ne * nw);
   int qp_log2 = 0, spt;
   if (!big) {
@@ -468,7 +468,6 @@ int mix_csr_pm_impl(const char* nm, const float* XT, int64_t ldx, int32_t x_rows
   };
   if (big && big_nb == 5) pick(integral_constant<int, 8192>{}, integral_constant<int, 5>{}, integral_constant<int, 2>{});
   else if (big) pick(integral_constant<int, 8192>{}, integral_constant<int, 4>{}, integral_constant<int, 2>{});
-  else if (small5) pick(integral_constant<int, 8192>{}, integral_constant<int, 5>{}, integral_constant<int, 1>{});
   else pick(integral_constant<int, 16384>{}, integral_constant<int, 2>{}, integral_constant<int, 1>{});
   return check_launch(nm);
 }
