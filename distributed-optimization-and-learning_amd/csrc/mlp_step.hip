@@ -36,6 +36,8 @@
 // consecutive W1 columns and W1 / momentum move as 16-B buffer ops, 4 + 4
 // per lane and tile instead of 16 + 16): 0.577-0.579 vs 0.505 ms; each 16-B
 // instruction then touches 32 W1 rows' lines instead of 2 (same profile): dropped.
+// dW1 compiled for >= 5 / 6 waves per SIMD (96 / 80 VGPRs, 20 / 84 B of
+// scratch) instead of 4 (104): 0.534 / 0.761 vs 0.506 ms (same profile).
 //   update (every parameter, as dol_prox_admm_sgd_f32):
 //       g' = g [+ (alpha +) rho*(w - theta)];  buf = mom*buf + g' (buf = g' on the
 //       first step);  w = fma(-lr, buf, w)
