@@ -38,6 +38,7 @@
 // (blockIdx % 8 = XCD), so the slab's chunks come from HBM once and from that
 // XCD's L2 for the others.
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <stdint.h>
 #include <stdlib.h>
 
@@ -94,35 +95,59 @@ __device__ __forceinline__ uint32_t piece_addr(uint32_t o, uint32_t lb) { return
 // index by scalar loads (2.1 ms).  Chunk headers (row starts, the next block's
 // bounds) arrive by vector loads issued with the chunk's DMA, so the chunk
 // loop has no scalar-load waits (1.105-1.12 vs 1.135-1.147 ms with s_load).
+// Work items: item t = (slab, row group) with t's low 3 bits = the XCD (t & 7),
+// slab = ((t >> 3) / n_rg) * 8 + (t & 7), rg = (t >> 3) % n_rg.  Workgroup b
+// takes items b, b + G, b + 2G, ... (G = gridDim.x, a multiple of 8, so every
+// item of a workgroup is on its XCD); with G = n_items each workgroup runs one
+// item.  Persistent (G < n_items): the chunk stream runs on across items — the
+// next item's chunk 0 is staged during the current item's last chunk, so a new
+// item does not start on an exposed DMA latency (needs nk >= 2).
 template <int PROBE = 0>
 __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
     const float* __restrict__ X, int64_t ldx, int x_rows, float* __restrict__ Y, int64_t ldy, int n_rows, int64_t P,
-    const int32_t* __restrict__ ent, const int32_t* __restrict__ hdr, int nk, int n_rg, int64_t n_slabs) {
+    const int32_t* __restrict__ ent, const int32_t* __restrict__ hdr, int nk, int n_rg, int64_t n_slabs,
+    int64_t n_items) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const uint32_t b = blockIdx.x;
-  const uint32_t xcd = b & 7u, local = b >> 3;
-  const int rg = int(local % uint32_t(n_rg));
-  const int64_t slab = int64_t(local / uint32_t(n_rg)) * 8 + xcd;
-  if (slab >= n_slabs) return;
+  const int64_t G = gridDim.x;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t p = slab * kCols + lane * 4;       // this lane's first column
-  const int64_t pl = p + 4 <= ldx ? p : ldx - 4;   // in-bounds DMA column (lanes past P: values unused)
-  const float* xsrc = X + pl;
-  const int32_t* H = hdr + int64_t(rg) * nk * (kRows + 1);  // this row group's blocks
+  struct Item {
+    int rg;
+    int64_t p;               // this lane's first column
+    const float* xsrc;       // X + the in-bounds DMA column of this lane
+    const int32_t* H;        // the row group's chunk blocks
+  };
+  auto item_at = [&](int64_t t, Item& it) -> bool {  // false: no such item (and none later for this workgroup)
+    if (t >= n_items) return false;
+    const uint32_t local = uint32_t(t >> 3);
+    const int64_t slab = int64_t(local / uint32_t(n_rg)) * 8 + (t & 7);
+    if (slab >= n_slabs) return false;
+    it.rg = int(local % uint32_t(n_rg));
+    it.p = slab * kCols + lane * 4;
+    const int64_t pl = it.p + 4 <= ldx ? it.p : ldx - 4;  // lanes past P: values unused
+    it.xsrc = X + pl;
+    it.H = hdr + int64_t(it.rg) * nk * (kRows + 1);
+    return true;
+  };
+  int64_t t = blockIdx.x;
+  Item cur, nxt;
+  if (!item_at(t, cur)) return;
+  bool has_next = item_at(t + G, nxt);
   const uint8_t* entb = reinterpret_cast<const uint8_t*>(ent);
 
   const int row0 = wave * kRW;  // within the group
-  int blk0 = H[0], blk1 = H[kRows];  // chunk 0's index block [blk0, blk1)
-  int hv = 0;                         // header lanes, see issue()
-  auto issue = [&](int k) {
+  int blk0 = cur.H[0], blk1 = cur.H[kRows];  // the next chunk to stage: its index block [blk0, blk1)
+  int hv = 0;                                 // header lanes, see issue()
+  // stage chunk k of item `it` into buffer `buf`; `after` = the item whose chunk 0
+  // follows it when k is the last chunk (nullptr: none)
+  auto issue = [&](const Item& it, int k, int buf, const Item* after) {
     if constexpr (PROBE == 2) return;
-    uint8_t* dst = lds + (k & 1) * kXBytes;
+    uint8_t* dst = lds + buf * kXBytes;
 #pragma unroll
     for (int i = 0; i < kPerWave; ++i) {
       const int al = wave * kPerWave + i;
       const int a = min(k * kChunk + al, x_rows - 1);  // agents past x_rows: never referenced
-      __builtin_amdgcn_global_load_lds(DOL_GPTR(xsrc + int64_t(a) * ldx), DOL_LPTR(dst + al * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(DOL_GPTR(it.xsrc + int64_t(a) * ldx), DOL_LPTR(dst + al * 1024), 16, 0, 0);
     }
     // the chunk's index block (16-B aligned start, whole 1 KiB pieces; ent is padded)
     const int64_t a0 = int64_t(blk0 & ~1) * 8;  // even: 16-B aligned
@@ -130,12 +155,14 @@ __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
     if (nbytes <= kIdxBytes)
       for (int pc = wave; pc * 1024 < nbytes; pc += kWaves)
         __builtin_amdgcn_global_load_lds(DOL_GPTR(entb + a0 + pc * 1024 + lane * 16),
-                                         DOL_LPTR(lds + kIdxBase + (k & 1) * kIdxBytes + pc * 1024), 16, 0, 0);
+                                         DOL_LPTR(lds + kIdxBase + buf * kIdxBytes + pc * 1024), 16, 0, 0);
     // headers ride the same vmcnt wait: lanes 0..kRW hold chunk k's row starts of
-    // this wave's rows, lanes kRW+1 / kRW+2 chunk k+1's block bounds
-    const int hl = lane <= kRW ? row0 + lane : (lane == kRW + 1 ? 0 : kRows);
-    const int kk = lane <= kRW ? k : min(k + 1, nk - 1);
-    if (lane <= kRW + 2) hv = H[int64_t(kk) * (kRows + 1) + hl];
+    // this wave's rows, lanes kRW+1 / kRW+2 the block bounds of the chunk after it
+    const int32_t* hb = it.H + int64_t(k + 1) * (kRows + 1);   // (it, k + 1)
+    if (k + 1 >= nk) hb = after ? after->H : it.H + int64_t(k) * (kRows + 1);  // (after, 0), or unused
+    if (lane <= kRW) hv = it.H[int64_t(k) * (kRows + 1) + row0 + lane];
+    else if (lane == kRW + 1) hv = hb[0];
+    else if (lane == kRW + 2) hv = hb[kRows];
   };
 
   f4 acc[kRW];
@@ -143,76 +170,91 @@ __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
   for (int r = 0; r < kRW; ++r) acc[r] = f4{0.f, 0.f, 0.f, 0.f};
   const uint32_t lane16 = uint32_t(lane) * 16;
 
-  issue(0);
-  for (int k = 0; k < nk; ++k) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // my pieces (and header lanes) of chunk k landed
-    __syncthreads();                                   // ... and every wave's; buffer (k+1)&1 is free
-    int bnd[kRW + 1];  // header words: (even) first entry | 1 if the row's segment ends in a pad entry
+  int g = 0;  // chunks consumed by this workgroup: buffer g & 1
+  issue(cur, 0, 0, has_next ? &nxt : nullptr);
+  for (;;) {
+    Item nn;  // the item after nxt (header bounds of nxt's last chunk)
+    const bool has_nn = has_next && item_at(t + 2 * G, nn);
+    for (int k = 0; k < nk; ++k, ++g) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // my pieces (and header lanes) of chunk k landed
+      __syncthreads();                                   // ... and every wave's; the other buffer is free
+      int bnd[kRW + 1];  // header words: (even) first entry | 1 if the row's segment ends in a pad entry
 #pragma unroll
-    for (int i = 0; i <= kRW; ++i) bnd[i] = __builtin_amdgcn_readlane(hv, i);
-    const int e0 = blk0 & ~1;
-    const bool fits = int64_t((blk1 & ~1) - e0) * 8 <= kIdxBytes;
-    blk0 = __builtin_amdgcn_readlane(hv, kRW + 1);  // chunk k+1's block, for issue(k + 1)
-    blk1 = __builtin_amdgcn_readlane(hv, kRW + 2);
-    if (k + 1 < nk) issue(k + 1);
-    if constexpr (PROBE == 1) continue;
-    const uint32_t lb = uint32_t((k & 1) * kXBytes) + lane16;  // stage base + my lane's 16 B
-    if (!fits) {  // an over-full block (denser graphs): indices from global memory, same order
+      for (int i = 0; i <= kRW; ++i) bnd[i] = __builtin_amdgcn_readlane(hv, i);
+      const int e0 = blk0 & ~1;
+      const bool fits = int64_t((blk1 & ~1) - e0) * 8 <= kIdxBytes;
+      blk0 = __builtin_amdgcn_readlane(hv, kRW + 1);  // the next chunk's block, for the issue below
+      blk1 = __builtin_amdgcn_readlane(hv, kRW + 2);
+      if (k + 1 < nk) issue(cur, k + 1, (g + 1) & 1, has_next ? &nxt : nullptr);
+      else if (has_next) issue(nxt, 0, (g + 1) & 1, has_nn ? &nn : nullptr);
+      if constexpr (PROBE == 1) continue;
+      const uint32_t lb = uint32_t((g & 1) * kXBytes) + lane16;  // stage base + my lane's 16 B
+      if (!fits) {  // an over-full block (denser graphs): indices from global memory, same order
+#pragma unroll
+        for (int r = 0; r < kRW; ++r) {
+          const int s = bnd[r] & ~1, n = (bnd[r + 1] & ~1) - s - (bnd[r] & 1);
+          for (int e = s; e < s + n; ++e)
+            acc[r] = fmac(acc[r], __int_as_float(ent[2 * int64_t(e) + 1]),
+                          *reinterpret_cast<const f4*>(lds + piece_addr(uint32_t(ent[2 * int64_t(e)]), lb)));
+        }
+        continue;
+      }
+      // the block in LDS as 16-B pairs of entries (every row segment starts on an
+      // even entry, so a pair never straddles two rows' segments): one uniform
+      // ds_read_b128 (4 LDS cycles) carries two (offset, weight) entries
+      const I4* ib4 = reinterpret_cast<const I4*>(lds + kIdxBase + (g & 1) * kIdxBytes);
+      auto gather = [&](uint32_t o) { return *reinterpret_cast<const f4*>(lds + piece_addr(o, lb)); };
 #pragma unroll
       for (int r = 0; r < kRW; ++r) {
-        const int s = bnd[r] & ~1, n = (bnd[r + 1] & ~1) - s - (bnd[r] & 1);
-        for (int e = s; e < s + n; ++e)
-          acc[r] = fmac(acc[r], __int_as_float(ent[2 * int64_t(e) + 1]),
-                        *reinterpret_cast<const f4*>(lds + piece_addr(uint32_t(ent[2 * int64_t(e)]), lb)));
+        const int s = (bnd[r] & ~1) - e0;  // pair-aligned, relative to the block
+        const int n = (bnd[r + 1] & ~1) - (bnd[r] & ~1) - (bnd[r] & 1);
+        f4 a = acc[r];
+        int j = 0;
+        for (; j + 4 <= n; j += 4) {
+          const I4 q0 = ib4[(s + j) >> 1], q1 = ib4[((s + j) >> 1) + 1];
+          const f4 x0 = gather(uint32_t(q0.x)), x1 = gather(uint32_t(q0.z));
+          const f4 x2 = gather(uint32_t(q1.x)), x3 = gather(uint32_t(q1.z));
+          a = fmac(a, __int_as_float(q0.y), x0);
+          a = fmac(a, __int_as_float(q0.w), x1);
+          a = fmac(a, __int_as_float(q1.y), x2);
+          a = fmac(a, __int_as_float(q1.w), x3);
+        }
+        if (j + 2 <= n) {
+          const I4 q0 = ib4[(s + j) >> 1];
+          const f4 x0 = gather(uint32_t(q0.x)), x1 = gather(uint32_t(q0.z));
+          a = fmac(a, __int_as_float(q0.y), x0);
+          a = fmac(a, __int_as_float(q0.w), x1);
+          j += 2;
+        }
+        if (j < n) {
+          const I4 q0 = ib4[(s + j) >> 1];
+          a = fmac(a, __int_as_float(q0.y), gather(uint32_t(q0.x)));
+        }
+        acc[r] = a;
       }
-      continue;
     }
-    // the block in LDS as 16-B pairs of entries (every row segment starts on an
-    // even entry, so a pair never straddles two rows' segments): one uniform
-    // ds_read_b128 (4 LDS cycles) carries two (offset, weight) entries
-    const I4* ib4 = reinterpret_cast<const I4*>(lds + kIdxBase + (k & 1) * kIdxBytes);
-    auto gather = [&](uint32_t o) { return *reinterpret_cast<const f4*>(lds + piece_addr(o, lb)); };
+    const int64_t p = cur.p;
+    if (p < P) {
+      const int grow0 = cur.rg * kRows + row0;
 #pragma unroll
-    for (int r = 0; r < kRW; ++r) {
-      const int s = (bnd[r] & ~1) - e0;  // pair-aligned, relative to the block
-      const int n = (bnd[r + 1] & ~1) - (bnd[r] & ~1) - (bnd[r] & 1);
-      f4 a = acc[r];
-      int j = 0;
-      for (; j + 4 <= n; j += 4) {
-        const I4 q0 = ib4[(s + j) >> 1], q1 = ib4[((s + j) >> 1) + 1];
-        const f4 x0 = gather(uint32_t(q0.x)), x1 = gather(uint32_t(q0.z));
-        const f4 x2 = gather(uint32_t(q1.x)), x3 = gather(uint32_t(q1.z));
-        a = fmac(a, __int_as_float(q0.y), x0);
-        a = fmac(a, __int_as_float(q0.w), x1);
-        a = fmac(a, __int_as_float(q1.y), x2);
-        a = fmac(a, __int_as_float(q1.w), x3);
+      for (int r = 0; r < kRW; ++r) {
+        if (grow0 + r < n_rows) {
+          float* y = Y + int64_t(grow0 + r) * ldy + p;
+          if (p + 4 <= P) {
+            __builtin_nontemporal_store(acc[r], reinterpret_cast<f4*>(y));
+          } else {
+            for (int c = 0; c < int(P - p); ++c) y[c] = acc[r][c];
+          }
+        }
       }
-      if (j + 2 <= n) {
-        const I4 q0 = ib4[(s + j) >> 1];
-        const f4 x0 = gather(uint32_t(q0.x)), x1 = gather(uint32_t(q0.z));
-        a = fmac(a, __int_as_float(q0.y), x0);
-        a = fmac(a, __int_as_float(q0.w), x1);
-        j += 2;
-      }
-      if (j < n) {
-        const I4 q0 = ib4[(s + j) >> 1];
-        a = fmac(a, __int_as_float(q0.y), gather(uint32_t(q0.x)));
-      }
-      acc[r] = a;
     }
-  }
-  if (p >= P) return;
-  const int grow0 = rg * kRows + row0;
+    if (!has_next) break;
 #pragma unroll
-  for (int r = 0; r < kRW; ++r) {
-    if (grow0 + r < n_rows) {
-      float* y = Y + int64_t(grow0 + r) * ldy + p;
-      if (p + 4 <= P) {
-        __builtin_nontemporal_store(acc[r], reinterpret_cast<f4*>(y));
-      } else {
-        for (int c = 0; c < int(P - p); ++c) y[c] = acc[r][c];
-      }
-    }
+    for (int r = 0; r < kRW; ++r) acc[r] = f4{0.f, 0.f, 0.f, 0.f};
+    t += G;
+    cur = nxt;
+    nxt = nn;
+    has_next = has_nn;
   }
 }
 
@@ -435,13 +477,24 @@ extern "C" int dol_mix_csr_slab_f32(const float* X, int64_t ldx, int32_t x_rows,
   const int nk = dol_csr_slab_nk(x_rows);
   const int64_t n_rg = cdiv(n_rows, kRows);
   const int64_t n_slabs = cdiv(P, kCols);
-  const int64_t grid = 8 * cdiv(n_slabs, 8) * n_rg;
-  if (grid >= (int64_t(1) << 32)) return fail(DOL_EINVAL, "dol_mix_csr_slab_f32: too many workgroups");
+  const int64_t n_items = 8 * cdiv(n_slabs, 8) * n_rg;
+  if (n_items >= (int64_t(1) << 32)) return fail(DOL_EINVAL, "dol_mix_csr_slab_f32: too many workgroups");
   static const int probe = [] { const char* e = getenv("DOL_SLAB_PROBE"); return e ? atoi(e) : 0; }();
+  // persistent grid (one workgroup per CU, a multiple of 8) unless DOL_SLAB_PERSIST=0
+  // or a single chunk (x_rows <= 64: the stream needs nk >= 2)
+  static const int persist = [] { const char* e = getenv("DOL_SLAB_PERSIST"); return e ? atoi(e) : 1; }();
+  static const int n_cu = [] {
+    int dev = 0, cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cu = 0;
+    return cu;
+  }();
+  const int64_t g_cap = int64_t(n_cu) / 8 * 8;
+  const int64_t grid = (persist && nk >= 2 && g_cap >= 8) ? std::min<int64_t>(n_items, g_cap) : n_items;
   auto launch = [&](auto kern) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, kLds);
     hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(grid)), dim3(kThreads), kLds, s, X, ldx, x_rows, Y, ldy,
-                       n_rows, P, ent, hdr, nk, static_cast<int>(n_rg), n_slabs);
+                       n_rows, P, ent, hdr, nk, static_cast<int>(n_rg), n_slabs, n_items);
   };
   if (probe == 1) launch(csr_slab_kernel<1>);
   else if (probe == 2) launch(csr_slab_kernel<2>);
