@@ -11,9 +11,10 @@
 // not bit-exact.  Here each X value is read from HBM once per row group and
 // from LDS once per (output row, neighbour):
 //
-//   * a workgroup (16 waves) owns one SLAB = 256 columns of P and a ROW GROUP
-//     of 16 * RW output rows, RW per wave, held in registers (f4 per row per
-//     lane: lane l owns columns 4l .. 4l+3 of the slab);
+//   * a work item is one SLAB = 256 columns of P and a ROW GROUP of 16 * RW
+//     output rows, RW per wave, held in registers (f4 per row per lane: lane l
+//     owns columns 4l .. 4l+3 of the slab); a workgroup (16 waves, one per CU)
+//     walks its items with the chunk stream running on across them;
 //   * the slab's X columns stream through LDS in CHUNKS of 64 agents (64 x 1 KiB,
 //     LDS-DMA global_load_lds_dwordx4: each agent's 1 KiB piece is contiguous
 //     in HBM and lands contiguous in LDS), double-buffered;
