@@ -27,11 +27,14 @@
 //     (in-order, ~120-cycle reads, prefetched a step ahead) instead of scalar
 //     loads from L2 (out-of-order returns force a full drain per use: measured
 //     2.1 ms vs 0.24 ms of staging at 1024 x 101,770);
-//   * four rows walk their chunk entries in lockstep, two per row per step:
-//     one conflict-free ds_read_b128 (1 KiB: the wave reads one agent's whole
-//     piece) + 4 separately rounded mul / add per neighbour.  Chunks are
-//     visited in ascending agent order, so each row's sum runs over its CSR
-//     entries in exactly the reference's order.
+//   * each wave walks its 8 rows' chunk segments as one contiguous run of
+//     entry PAIRS (pads included: a pad reads a zero piece and adds +0), the
+//     next two pairs always in flight behind the current pairs' gathers: per
+//     entry one conflict-free ds_read_b128 gather (1 KiB: the wave reads one
+//     agent's whole piece) + 4 separately rounded mul / add, per pair one
+//     uniform ds_read_b128 of the index.  Chunks are visited in ascending agent
+//     order, so each row's sum runs over its CSR entries in exactly the
+//     reference's order.
 //
 // Bounds: LDS bytes = nnz * 1 KiB per slab (256 B/clk/CU), VALU = 5 wave
 // instructions per (neighbour, slab) (address add, 2 packed mul, 2 packed
@@ -55,22 +58,44 @@ constexpr int kChunk = DOL_SLAB_CHUNK;     // agents per LDS chunk
 constexpr int kWaves = 16;
 constexpr int kThreads = 64 * kWaves;
 constexpr int kXBytes = kChunk * kCols * 4;  // 64 KiB of X per chunk
-constexpr int kIdxBytes = 16 * 1024;          // index block capacity per chunk (2048 entries)
-// LDS: X stages at 0 and 64 KiB, index stages at 128 KiB and 144 KiB: 160 KiB
-constexpr int kIdxBase = 2 * kXBytes;
-constexpr int kLds = 2 * kXBytes + 2 * kIdxBytes;
+// LDS: stage b = X chunk (64 KiB) + one zero piece (1 KiB) at b * kStage; the
+// two index stages (15 KiB each) after them: 2 * 65 + 2 * 15 = 160 KiB.  A pad
+// entry's offset is kZeroRel, i.e. the zero piece of whichever stage it is read
+// against, with weight 0: its product is +0 and acc + (+0) == acc for every
+// acc the sum can hold (+0 start, round-to-nearest never yields -0 from +0),
+// so pads are gathered like real entries and leave the bits unchanged.
+constexpr int kStage = kXBytes + 1024;
+constexpr int kZeroRel = kXBytes;
+constexpr int kIdxBytes = 15 * 1024;          // index block capacity per chunk (1920 entries)
+constexpr int kIdxBase = 2 * kStage;
+constexpr int kLds = 2 * kStage + 2 * kIdxBytes;
+constexpr int kAhead = 32;                    // index bytes a wave reads past its stream (two pairs)
 constexpr int kRW = 8;                        // rows per wave
 constexpr int kRows = kWaves * kRW;           // rows per row group
 constexpr int kEntPad = 160;                  // ent pad entries (the block DMA may read 1 KiB + 8 B past a block)
 constexpr int kPerWave = kChunk / kWaves;  // DMA pieces per wave per chunk
 static_assert(kChunk % kWaves == 0, "chunk must split evenly over the waves");
+static_assert(kLds <= 160 * 1024, "LDS budget");
 
 #define DOL_GPTR(p) ((const __attribute__((address_space(1))) void*)(p))
 #define DOL_LPTR(p) ((__attribute__((address_space(3))) void*)(p))
 
 struct alignas(16) I4 {
-  int32_t x, y, z, w;  // two (LDS byte offset of the neighbour's piece in its chunk, weight bits) entries
+  int32_t x, y, z, w;  // a PAIR of entries: (offset 0, offset 1, weight bits 0, weight bits 1)
 };
+
+// LDS-DMA of 16 B per lane (1 KiB per wave) from `gptr` to the wave-uniform LDS
+// address of `ldst` (the hardware adds lane * 16), written as inline asm: the
+// compiler's waitcnt model treats a pending global_load_lds as making LGKM
+// returns unordered and then waits lgkmcnt(0) before every LDS read result is
+// used, which serialises the gather pipeline below; hidden from it, the gathers
+// get counted lgkmcnt waits.  The kernel orders the DMA itself (s_waitcnt
+// vmcnt(0) + barrier before a stage is read); any compiler-counted vmcnt wait
+// issued later only waits for more, never fewer, loads.
+__device__ __forceinline__ void dma16(const void* gptr, void* ldst) {
+  const uint32_t la = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(DOL_LPTR(ldst)));
+  asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(gptr), "{m0}"(__builtin_amdgcn_readfirstlane(la)) : "memory");
+}
 
 // separately rounded mul, then add (v_pk_mul_f32 / v_pk_add_f32 pairs: 1.18 ms
 // vs 1.33 with the per-component scalar form at 1024 x 101,770, same bits)
@@ -79,8 +104,9 @@ __device__ __forceinline__ f4 fmac(f4 acc, float w, f4 x) { return acc + x * w; 
 // LDS byte address of entry word `o`'s piece for this lane (stage base + lane * 16 in `lb`)
 __device__ __forceinline__ uint32_t piece_addr(uint32_t o, uint32_t lb) { return o + lb; }
 
-// PROBE (diagnostics, DOL_SLAB_PROBE): 1 = staging only (no gathers), 2 = gathers
-// only (no LDS-DMA: sums of whatever LDS holds; results meaningless).
+// PROBE (diagnostics, DOL_SLAB_PROBE; results meaningless except 0): 1 = staging
+// only (no gathers), 2 = no X staging (index blocks and gathers only), 3 = no
+// workgroup barrier per chunk (waves drift; reads race the DMA).
 // Each row walks its chunk segment in groups of 4 / 2 / 1 entries: the index
 // pairs by uniform ds_read_b128 (segments are padded to even lengths, so two
 // entries share one 16-B LDS read: 2 LDS cycles per entry; ds_read2_b64 took
@@ -110,6 +136,7 @@ __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
     int64_t n_items) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int64_t G = gridDim.x;
+  const int64_t p4 = (P + 3) / 4 * 4;  // X rows are readable up to here (dol_hip.h)
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   struct Item {
@@ -125,7 +152,7 @@ __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
     if (slab >= n_slabs) return false;
     it.rg = int(local % uint32_t(n_rg));
     it.p = slab * kCols + lane * 4;
-    const int64_t pl = it.p + 4 <= ldx ? it.p : ldx - 4;  // lanes past P: values unused
+    const int64_t pl = it.p + 4 <= p4 ? it.p : p4 - 4;  // lanes past P: values unused, reads kept inside round_up(P, 4)
     it.xsrc = X + pl;
     it.H = hdr + int64_t(it.rg) * nk * (kRows + 1);
     return true;
@@ -142,21 +169,19 @@ __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
   // stage chunk k of item `it` into buffer `buf`; `after` = the item whose chunk 0
   // follows it when k is the last chunk (nullptr: none)
   auto issue = [&](const Item& it, int k, int buf, const Item* after) {
-    if constexpr (PROBE == 2) return;
-    uint8_t* dst = lds + buf * kXBytes;
+    uint8_t* dst = lds + buf * kStage;
 #pragma unroll
-    for (int i = 0; i < kPerWave; ++i) {
+    for (int i = 0; i < kPerWave && PROBE != 2; ++i) {
       const int al = wave * kPerWave + i;
       const int a = min(k * kChunk + al, x_rows - 1);  // agents past x_rows: never referenced
-      __builtin_amdgcn_global_load_lds(DOL_GPTR(it.xsrc + int64_t(a) * ldx), DOL_LPTR(dst + al * 1024), 16, 0, 0);
+      dma16(it.xsrc + int64_t(a) * ldx, dst + al * 1024);
     }
     // the chunk's index block (16-B aligned start, whole 1 KiB pieces; ent is padded)
     const int64_t a0 = int64_t(blk0 & ~1) * 8;  // even: 16-B aligned
     const int64_t nbytes = int64_t(blk1 & ~1) * 8 - a0;
-    if (nbytes <= kIdxBytes)
+    if (nbytes <= kIdxBytes - kAhead)
       for (int pc = wave; pc * 1024 < nbytes; pc += kWaves)
-        __builtin_amdgcn_global_load_lds(DOL_GPTR(entb + a0 + pc * 1024 + lane * 16),
-                                         DOL_LPTR(lds + kIdxBase + buf * kIdxBytes + pc * 1024), 16, 0, 0);
+        dma16(entb + a0 + pc * 1024 + lane * 16, lds + kIdxBase + buf * kIdxBytes + pc * 1024);
     // headers ride the same vmcnt wait: lanes 0..kRW hold chunk k's row starts of
     // this wave's rows, lanes kRW+1 / kRW+2 the block bounds of the chunk after it
     const int32_t* hb = it.H + int64_t(k + 1) * (kRows + 1);   // (it, k + 1)
@@ -170,6 +195,8 @@ __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
 #pragma unroll
   for (int r = 0; r < kRW; ++r) acc[r] = f4{0.f, 0.f, 0.f, 0.f};
   const uint32_t lane16 = uint32_t(lane) * 16;
+  if (threadIdx.x < 128)  // the two stages' zero pieces (pads read them); visible after the first barrier
+    *reinterpret_cast<f4*>(lds + (threadIdx.x >> 6) * kStage + kZeroRel + lane16) = f4{0.f, 0.f, 0.f, 0.f};
 
   int g = 0;  // chunks consumed by this workgroup: buffer g & 1
   issue(cur, 0, 0, has_next ? &nxt : nullptr);
@@ -178,58 +205,62 @@ __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
     const bool has_nn = has_next && item_at(t + 2 * G, nn);
     for (int k = 0; k < nk; ++k, ++g) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // my pieces (and header lanes) of chunk k landed
-      __syncthreads();                                   // ... and every wave's; the other buffer is free
+      if constexpr (PROBE != 3) __syncthreads();         // ... and every wave's; the other buffer is free
       int bnd[kRW + 1];  // header words: (even) first entry | 1 if the row's segment ends in a pad entry
 #pragma unroll
-      for (int i = 0; i <= kRW; ++i) bnd[i] = __builtin_amdgcn_readlane(hv, i);
+      for (int i = 0; i <= kRW; ++i) bnd[i] = __builtin_amdgcn_readlane(hv, i) & ~1;
       const int e0 = blk0 & ~1;
-      const bool fits = int64_t((blk1 & ~1) - e0) * 8 <= kIdxBytes;
+      const bool fits = int64_t((blk1 & ~1) - e0) * 8 <= kIdxBytes - kAhead;
       blk0 = __builtin_amdgcn_readlane(hv, kRW + 1);  // the next chunk's block, for the issue below
       blk1 = __builtin_amdgcn_readlane(hv, kRW + 2);
       if (k + 1 < nk) issue(cur, k + 1, (g + 1) & 1, has_next ? &nxt : nullptr);
       else if (has_next) issue(nxt, 0, (g + 1) & 1, has_nn ? &nn : nullptr);
       if constexpr (PROBE == 1) continue;
-      const uint32_t lb = uint32_t((g & 1) * kXBytes) + lane16;  // stage base + my lane's 16 B
+      const uint32_t lb = uint32_t((g & 1) * kStage) + lane16;  // stage base + my lane's 16 B
+      auto gather = [&](int32_t o) { return *reinterpret_cast<const f4*>(lds + piece_addr(uint32_t(o), lb)); };
       if (!fits) {  // an over-full block (denser graphs): indices from global memory, same order
 #pragma unroll
-        for (int r = 0; r < kRW; ++r) {
-          const int s = bnd[r] & ~1, n = (bnd[r + 1] & ~1) - s - (bnd[r] & 1);
-          for (int e = s; e < s + n; ++e)
-            acc[r] = fmac(acc[r], __int_as_float(ent[2 * int64_t(e) + 1]),
-                          *reinterpret_cast<const f4*>(lds + piece_addr(uint32_t(ent[2 * int64_t(e)]), lb)));
-        }
+        for (int r = 0; r < kRW; ++r)
+          for (int e = bnd[r]; e < bnd[r + 1]; ++e) {
+            const int64_t q = int64_t(e >> 1) * 4 + (e & 1);
+            acc[r] = fmac(acc[r], __int_as_float(ent[q + 2]), gather(ent[q]));
+          }
         continue;
       }
-      // the block in LDS as 16-B pairs of entries (every row segment starts on an
-      // even entry, so a pair never straddles two rows' segments): one uniform
-      // ds_read_b128 (4 LDS cycles) carries two (offset, weight) entries
-      const I4* ib4 = reinterpret_cast<const I4*>(lds + kIdxBase + (g & 1) * kIdxBytes);
-      auto gather = [&](uint32_t o) { return *reinterpret_cast<const f4*>(lds + piece_addr(o, lb)); };
+      // This wave's rows' segments are one contiguous run of entry pairs in the
+      // block (row order; every segment an even number of entries, pads
+      // included).  The wave walks it with the next two pairs always in flight:
+      // one uniform ds_read_b128 per pair (2 LDS cycles per entry), read while
+      // the current pairs' gathers are outstanding, so each step waits on one
+      // LDS round trip (the gathers) instead of two.  The run may be read up to
+      // kAhead bytes past its end (inside the stage: `fits` leaves the room).
+      uint32_t ip = uint32_t(kIdxBase + (g & 1) * kIdxBytes + (bnd[0] - e0) * 8);
+      auto pair_at = [&](uint32_t a) { return *static_cast<const I4*>(__builtin_assume_aligned(lds + a, 16)); };
+      I4 qa = pair_at(ip), qb = pair_at(ip + 16);
+      ip += 32;
 #pragma unroll
       for (int r = 0; r < kRW; ++r) {
-        const int s = (bnd[r] & ~1) - e0;  // pair-aligned, relative to the block
-        const int n = (bnd[r + 1] & ~1) - (bnd[r] & ~1) - (bnd[r] & 1);
+        int np = (bnd[r + 1] - bnd[r]) >> 1;  // pairs of row r in this chunk
         f4 a = acc[r];
-        int j = 0;
-        for (; j + 4 <= n; j += 4) {
-          const I4 q0 = ib4[(s + j) >> 1], q1 = ib4[((s + j) >> 1) + 1];
-          const f4 x0 = gather(uint32_t(q0.x)), x1 = gather(uint32_t(q0.z));
-          const f4 x2 = gather(uint32_t(q1.x)), x3 = gather(uint32_t(q1.z));
-          a = fmac(a, __int_as_float(q0.y), x0);
-          a = fmac(a, __int_as_float(q0.w), x1);
-          a = fmac(a, __int_as_float(q1.y), x2);
-          a = fmac(a, __int_as_float(q1.w), x3);
+        for (; np >= 2; np -= 2) {
+          const f4 x0 = gather(qa.x), x1 = gather(qa.y), x2 = gather(qb.x), x3 = gather(qb.y);
+          const I4 na = pair_at(ip), nb = pair_at(ip + 16);
+          ip += 32;
+          a = fmac(a, __int_as_float(qa.z), x0);
+          a = fmac(a, __int_as_float(qa.w), x1);
+          a = fmac(a, __int_as_float(qb.z), x2);
+          a = fmac(a, __int_as_float(qb.w), x3);
+          qa = na;
+          qb = nb;
         }
-        if (j + 2 <= n) {
-          const I4 q0 = ib4[(s + j) >> 1];
-          const f4 x0 = gather(uint32_t(q0.x)), x1 = gather(uint32_t(q0.z));
-          a = fmac(a, __int_as_float(q0.y), x0);
-          a = fmac(a, __int_as_float(q0.w), x1);
-          j += 2;
-        }
-        if (j < n) {
-          const I4 q0 = ib4[(s + j) >> 1];
-          a = fmac(a, __int_as_float(q0.y), gather(uint32_t(q0.x)));
+        if (np) {
+          const f4 x0 = gather(qa.x), x1 = gather(qa.y);
+          const I4 nb = pair_at(ip);
+          ip += 16;
+          a = fmac(a, __int_as_float(qa.z), x0);
+          a = fmac(a, __int_as_float(qa.w), x1);
+          qa = qb;
+          qb = nb;
         }
         acc[r] = a;
       }
@@ -428,8 +459,9 @@ __global__ __launch_bounds__(64) void slab_scatter_kernel(const int32_t* __restr
     const int c = col[e], k = c / kChunk;
     const int first = lower_bound_col(col, e0, e1, k * kChunk);
     const int64_t dst = hdr[(int64_t(g) * nk + k) * (kRows + 1) + i] + (e - first);
-    ent[2 * dst] = (c % kChunk) * (kCols * 4);
-    ent[2 * dst + 1] = __float_as_int(val[e]);
+    const int64_t q = (dst >> 1) * 4 + (dst & 1);  // pair layout (off0, off1, w0, w1)
+    ent[q] = (c % kChunk) * (kCols * 4);
+    ent[q + 2] = __float_as_int(val[e]);
   }
   __syncthreads();  // every header read above is done before the pad bits change them
   for (int k = int(threadIdx.x); k < nk; k += 64) {
@@ -437,9 +469,10 @@ __global__ __launch_bounds__(64) void slab_scatter_kernel(const int32_t* __restr
     const int n = lower_bound_col(col, lo, e1, (k + 1) * kChunk) - lo;
     if (n & 1) {
       int32_t* h = hdr + (int64_t(g) * nk + k) * (kRows + 1) + i;
-      const int64_t pad = *h + n;
-      ent[2 * pad] = 0;
-      ent[2 * pad + 1] = 0;
+      const int64_t pad = *h + n;  // odd: the second slot of the segment's last pair
+      const int64_t q = (pad >> 1) * 4 + 1;
+      ent[q] = kZeroRel;
+      ent[q + 2] = 0;
       *h |= 1;
     }
   }
@@ -499,6 +532,7 @@ extern "C" int dol_mix_csr_slab_f32(const float* X, int64_t ldx, int32_t x_rows,
   };
   if (probe == 1) launch(csr_slab_kernel<1>);
   else if (probe == 2) launch(csr_slab_kernel<2>);
+  else if (probe == 3) launch(csr_slab_kernel<3>);
   else launch(csr_slab_kernel<0>);
   return dol::check_launch("dol_mix_csr_slab_f32");
 }

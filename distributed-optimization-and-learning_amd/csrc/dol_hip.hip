@@ -244,6 +244,29 @@ __global__ __launch_bounds__(kThreads) void ring_mix_kernel(
 
 
 
+// The two boundary rows of a sharded ring block in ONE launch (the multi-GPU
+// round, dolhip.parallel.ShardedRing: the interior rows are mixed while the
+// halo rows travel, then these two): blockIdx.y = 0 -> row 0 (previous row =
+// halo_prev), 1 -> row n_rows - 1 (next row = halo_next); with n_rows == 1 only
+// y = 0 runs and uses both halos.  Same arithmetic as ring_mix_kernel.
+template <typename V, class Epi = NoEpi>
+__global__ __launch_bounds__(kThreads) void ring_edges_kernel(
+    const float* __restrict__ X, int64_t ldx, float* __restrict__ Y, int64_t ldy, int n_rows, int64_t c_off,
+    int64_t ncols_v, const float* __restrict__ halo_prev, const float* __restrict__ halo_next,
+    const float* __restrict__ wprev, const float* __restrict__ wnext, Epi epi) {
+  const int64_t c = int64_t(blockIdx.x) * kThreads + threadIdx.x;
+  if (c >= ncols_v) return;
+  const int r = blockIdx.y == 0 ? 0 : n_rows - 1;
+  const float* pv = r == 0 ? halo_prev : X + int64_t(r - 1) * ldx;
+  const float* nx = r == n_rows - 1 ? halo_next : X + int64_t(r + 1) * ldx;
+  const V a = reinterpret_cast<const V*>(pv + c_off)[c];
+  const V b = reinterpret_cast<const V*>(nx + c_off)[c];
+  V out = axpy0(wprev[r], a, wnext[r], b);
+  const int64_t cf = c_off + c * Vec<V>::W;
+  out = epi.apply(out, epi.template load<V>(r, cf), r, cf);
+  reinterpret_cast<V*>(Y + int64_t(r) * ldy + c_off)[c] = out;
+}
+
 // LDS-DMA form of the ring mix (the default float4 path).  Each wave moves
 // its 1 KiB quarter of the tile's R + 2 rows straight into LDS with
 // global_load_lds_dwordx4 (default cache policy: the halo rows' second reads
@@ -1137,6 +1160,30 @@ int mix_ring_impl(const char* nm, const float* X, int64_t ldx, float* Y, int64_t
   return check_launch(nm);
 }
 
+template <class Epi>
+int ring_edges_impl(const char* nm, const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t n_rows, int64_t P,
+                    const float* halo_prev, const float* halo_next, const float* w_prev, const float* w_next,
+                    const Epi& epi, bool epi_vec_ok, hipStream_t s) {
+  if (n_rows < 0 || P < 0) return fail(DOL_EINVAL, "%s: negative size", nm);
+  if (n_rows == 0 || P == 0) { g_err[0] = '\0'; return DOL_OK; }
+  if (!X || !Y || !w_prev || !w_next || !halo_prev || !halo_next) return fail(DOL_EINVAL, "%s: null pointer", nm);
+  if (ldx < P || ldy < P) return fail(DOL_EINVAL, "%s: ld < P", nm);
+  if (X == Y) return fail(DOL_EINVAL, "%s: X and Y alias (Jacobi mix needs two buffers)", nm);
+  const bool vec_ok = row_vec_ok(X, ldx) && row_vec_ok(Y, ldy) && aligned16(halo_prev) && aligned16(halo_next) &&
+                      epi_vec_ok;
+  const ColSplit cs = split_cols(P, vec_ok);
+  const unsigned ny = n_rows == 1 ? 1u : 2u;
+  if (cs.n4 > 0)
+    hipLaunchKernelGGL((ring_edges_kernel<f4, Epi>), dim3(static_cast<unsigned>(cdiv(cs.n4, kThreads)), ny),
+                       dim3(kThreads), 0, s, X, ldx, Y, ldy, n_rows, int64_t(0), cs.n4, halo_prev, halo_next, w_prev,
+                       w_next, epi);
+  if (cs.tail > 0)
+    hipLaunchKernelGGL((ring_edges_kernel<float, Epi>), dim3(static_cast<unsigned>(cdiv(cs.tail, kThreads)), ny),
+                       dim3(kThreads), 0, s, X, ldx, Y, ldy, n_rows, cs.n4 * 4, cs.tail, halo_prev, halo_next, w_prev,
+                       w_next, epi);
+  return check_launch(nm);
+}
+
 }  // namespace
 
 // ============================================================================
@@ -1161,6 +1208,14 @@ int dol_mix_ring_f32(const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t
   DOL_DIMS_OK("dol_mix_ring_f32", ldx, ldy, P);
   return mix_ring_impl("dol_mix_ring_f32", X, ldx, Y, ldy, n_rows, P, halo_prev, halo_next, w_prev, w_next,
                        NoEpi{}, true, s);
+}
+
+int dol_mix_ring_edges_f32(const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t n_rows, int64_t P,
+                           const float* halo_prev, const float* halo_next, const float* w_prev,
+                           const float* w_next, hipStream_t s) {
+  DOL_DIMS_OK("dol_mix_ring_edges_f32", ldx, ldy, P);
+  return ring_edges_impl("dol_mix_ring_edges_f32", X, ldx, Y, ldy, n_rows, P, halo_prev, halo_next, w_prev, w_next,
+                         NoEpi{}, true, s);
 }
 
 }  // extern "C"
@@ -1217,6 +1272,24 @@ int dol_dgd_ring_f32(const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t
   }
   return with_dgd_epi(d, mode, [&](auto epi) {
     return mix_ring_impl(nm, X, ldx, Y, ldy, n_rows, P, halo_prev, halo_next, w_prev, w_next, epi, evec, s);
+  });
+}
+
+int dol_dgd_ring_edges_f32(const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t n_rows, int64_t P,
+                           const float* halo_prev, const float* halo_next, const float* w_prev, const float* w_next,
+                           const float* target, int64_t ldt, float* mom, int64_t ldm, int32_t objective,
+                           int32_t local_steps, float lr, float momentum, int first_step, hipStream_t s) {
+  DOL_DIMS_OK("dol_dgd_ring_edges_f32", ldx, ldy, P, ldt, ldm);
+  const char* nm = "dol_dgd_ring_edges_f32";
+  const DgdArgs d{target, ldt, mom, ldm, objective, local_steps, lr, momentum, first_step};
+  bool evec = false;
+  int mode = 0;
+  if (n_rows > 0 && P > 0) {
+    const int rc = check_dgd(nm, d, P, &evec, &mode);
+    if (rc) return rc;
+  }
+  return with_dgd_epi(d, mode, [&](auto epi) {
+    return ring_edges_impl(nm, X, ldx, Y, ldy, n_rows, P, halo_prev, halo_next, w_prev, w_next, epi, evec, s);
   });
 }
 

@@ -35,6 +35,9 @@ SIGNATURES = {
     "dol_mix_ring_steps_f32": [_ptr, _i64, _ptr, _i64, _i32, _i64, _i32, _ptr, _ptr, _ptr],
     "dol_mix_dense_f32": [_ptr, _i64, _ptr, _i64, _ptr, _i64, _i32, _i32, _i64, _ptr],
     "dol_mix_ring_f32": [_ptr, _i64, _ptr, _i64, _i32, _i64, _ptr, _ptr, _ptr, _ptr, _ptr],
+    "dol_mix_ring_edges_f32": [_ptr, _i64, _ptr, _i64, _i32, _i64, _ptr, _ptr, _ptr, _ptr, _ptr],
+    "dol_dgd_ring_edges_f32": [_ptr, _i64, _ptr, _i64, _i32, _i64, _ptr, _ptr, _ptr, _ptr, _ptr, _i64, _ptr, _i64,
+                               _i32, _i32, _f32, _f32, ctypes.c_int, _ptr],
     "dol_prox_admm_sgd_f32": [_ptr, _i64, _ptr, _i64, _ptr, _i64, _ptr, _ptr, _i64, _f32, _f32, _f32,
                               ctypes.c_int, ctypes.c_int, _i32, _i64, _ptr],
     "dol_admm_step_dual_f32": [_ptr, _i64, _ptr, _i64, _ptr, _i64, _ptr, _ptr, _i64, _f32, _f32, _f32,

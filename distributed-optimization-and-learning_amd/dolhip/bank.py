@@ -180,6 +180,18 @@ class AgentBank:
         alpha = self.buffer("alpha", zero=True)[sl] if admm else None
         ops.prox_admm_sgd(x, g, buf=buf, theta=theta, alpha=alpha, rho=rho, lr=lr, momentum=momentum,
                           first_step=first_step, write_grad=write_grad, P=self.P)
+        if momentum != 0.0:
+            self.mark_momentum_started(sl)
+
+    def mark_momentum_started(self, agents: slice) -> None:
+        """Record that rows `agents` have taken a momentum step (the batched
+        paths bypass the per-row optimizer, so they set the flags here)."""
+        a, b, st = agents.indices(self.n)
+        if st == 1 and not all(self.mom_started[a:b]):
+            self.mom_started[a:b] = [True] * max(0, b - a)
+        elif st != 1:
+            for i in range(a, b, st):
+                self.mom_started[i] = True
 
     def dual_update(self, theta: torch.Tensor, rho: float, resid_sq: Optional[torch.Tensor] = None,
                     agents: Optional[slice] = None) -> None:

@@ -390,7 +390,10 @@ class MixingPlan:
         'dense' plan on the matrix cores (tolerance path).  dense_kernel 'csr':
         the Neighbors selection runs on the device (dol_dense_to_csr_f32) and
         the plan mixes bit-exactly with the LDS-gather CSR kernel; `reuse` (a
-        previous 'csr' plan of the same shape) lends its buffers."""
+        previous 'csr' plan of the same shape) lends its buffers and is retired
+        (mixing with it afterwards raises).  The lent col / val buffers are sized
+        n_rows * n_cols (a dense W's worst case), so a reused plan never
+        reallocates whatever the round's W."""
         if W.device.type != "cuda" or W.dtype != torch.float32 or W.dim() != 2:
             raise ValueError("from_dense: expected a 2-D float32 CUDA tensor")
         if dense_kernel not in cls.DENSE_KERNELS + ("csr",):
@@ -414,7 +417,18 @@ class MixingPlan:
         plan.rowptr, plan.col, plan.val = ops.dense_to_csr(plan.W, *bufs)
         plan.ent, plan.hdr = ops.csr_slab_pack(plan.rowptr, plan.col, plan.val, plan.n_cols,
                                                *((reuse.ent, reuse.hdr) if same else (None, None)))
+        if same:  # the lender's buffers now hold this W: it must not mix again
+            reuse._retire()
         return plan
+
+    def _retire(self) -> None:
+        self.kind = "stale"
+        self.rowptr = self.col = self.val = self.ent = self.hdr = self.W = None
+
+    def _check_live(self) -> None:
+        if self.kind == "stale":
+            raise RuntimeError("this MixingPlan lent its buffers to a newer from_dense(..., reuse=plan) plan "
+                               "and no longer holds its W")
 
     @classmethod
     def from_graph(cls, W: Graph, device, allow_ring: bool = True, dense: bool = False,
@@ -454,6 +468,7 @@ class MixingPlan:
         return 1
 
     def _check_x(self, X: torch.Tensor) -> None:
+        self._check_live()
         need = self.n_cols
         if X.shape[0] < need:
             raise ValueError(f"X has {X.shape[0]} rows; W has {need} columns")

@@ -105,6 +105,8 @@ class BatchedMLP:
                      mom=b.buffer("mom", zero=True) if momentum != 0.0 else None,
                      theta=theta, alpha=b.buffer("alpha", zero=True) if admm else None, loss=loss,
                      lr=lr, momentum=momentum, rho=rho, first_step=first_step, update=True)
+        if momentum != 0.0:
+            b.mark_momentum_started(slice(0, b.n))
         return loss
 
     def step_unfused(self, X: torch.Tensor, y: torch.Tensor, lr: float, momentum: float, first_step: bool,

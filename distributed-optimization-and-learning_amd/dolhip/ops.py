@@ -15,7 +15,7 @@ from ._native import DolNativeError
 
 __all__ = [
     "DolNativeError", "mix_csr", "mix_ring", "mix_dense", "mix_dense_split3", "dense_split3_workspace_bytes", "split3_x_flags", "er_stochastic",
-    "mix_ring_steps", "prox_admm_sgd", "admm_dual", "ordered_mean",
+    "mix_ring_steps", "mix_ring_edges", "dgd_ring_edges", "prox_admm_sgd", "admm_dual", "ordered_mean",
     "ordered_sum", "stream_copy", "dual_workspace_bytes", "prox_grad", "admm_step_dual", "mlp_step",
     "dgd_ring", "dgd_csr", "OBJECTIVES", "admm_ls_round", "admm_ls_round_workspace_bytes", "mix_csr_pm",
     "transpose", "PM_MAX_AGENTS", "stream_copy_rows", "dgd_csr_pm", "PM_DGD_MAX_AGENTS",
@@ -464,6 +464,60 @@ def mix_ring(X: torch.Tensor, Y: torch.Tensor, w_prev: torch.Tensor, w_next: tor
         raise ValueError("X and Y alias: the Jacobi mix needs two buffers")
     _native.call("dol_mix_ring_f32", X.data_ptr(), ldx, Y.data_ptr(), ldy, n, P, _ptr(halo_prev),
                  _ptr(halo_next), w_prev.data_ptr(), w_next.data_ptr(), _stream(X))
+    return Y
+
+
+def mix_ring_edges(X: torch.Tensor, Y: torch.Tensor, w_prev: torch.Tensor, w_next: torch.Tensor,
+                   halo_prev: torch.Tensor, halo_next: torch.Tensor, P: Optional[int] = None,
+                   n_rows: Optional[int] = None) -> torch.Tensor:
+    """Rows 0 and n_rows-1 of mix_ring with halos, in one launch (the second
+    half of a sharded ring round; dol_mix_ring_edges_f32)."""
+    P = X.shape[1] if P is None else P
+    n = X.shape[0] if n_rows is None else n_rows
+    ldx = _check_rows("X", X, P)
+    ldy = _check_rows("Y", Y, P)
+    if X.shape[0] < n or Y.shape[0] < n:
+        raise ValueError("X/Y have fewer rows than n_rows")
+    for nm, t in (("w_prev", w_prev), ("w_next", w_next)):
+        if t.device != X.device or t.dtype != torch.float32 or t.numel() < n or not t.is_contiguous():
+            raise ValueError(f"{nm}: expected contiguous float32 [{n}] on {X.device}")
+    if halo_prev is None or halo_next is None:
+        raise ValueError("mix_ring_edges needs both halos")
+    _check_vec("halo_prev", halo_prev, P, X.device)
+    _check_vec("halo_next", halo_next, P, X.device)
+    if X.data_ptr() == Y.data_ptr():
+        raise ValueError("X and Y alias: the Jacobi mix needs two buffers")
+    _native.call("dol_mix_ring_edges_f32", X.data_ptr(), ldx, Y.data_ptr(), ldy, n, P, halo_prev.data_ptr(),
+                 halo_next.data_ptr(), w_prev.data_ptr(), w_next.data_ptr(), _stream(X))
+    return Y
+
+
+def dgd_ring_edges(X: torch.Tensor, Y: torch.Tensor, w_prev: torch.Tensor, w_next: torch.Tensor,
+                   target: torch.Tensor, halo_prev: torch.Tensor, halo_next: torch.Tensor,
+                   mom: Optional[torch.Tensor] = None, objective: str = "least_squares", steps: int = 1,
+                   lr: float = 0.01, momentum: float = 0.0, first_step: bool = False, P: Optional[int] = None,
+                   n_rows: Optional[int] = None) -> torch.Tensor:
+    """Rows 0 and n_rows-1 of dgd_ring with halos, in one launch (dol_dgd_ring_edges_f32)."""
+    P = X.shape[1] if P is None else P
+    n = X.shape[0] if n_rows is None else n_rows
+    ldx = _check_rows("X", X, P)
+    ldy = _check_rows("Y", Y, P)
+    if X.shape[0] < n or Y.shape[0] < n:
+        raise ValueError("X/Y have fewer rows than n_rows")
+    for nm, t in (("w_prev", w_prev), ("w_next", w_next)):
+        if t.device != X.device or t.dtype != torch.float32 or t.numel() < n or not t.is_contiguous():
+            raise ValueError(f"{nm}: expected contiguous float32 [{n}] on {X.device}")
+    if halo_prev is None or halo_next is None:
+        raise ValueError("dgd_ring_edges needs both halos")
+    _check_vec("halo_prev", halo_prev, P, X.device)
+    _check_vec("halo_next", halo_next, P, X.device)
+    if X.data_ptr() == Y.data_ptr():
+        raise ValueError("X and Y alias: the Jacobi mix needs two buffers")
+    ldt, ldm = _dgd_args(X, target, mom, objective, steps, momentum, P, n)
+    _native.call("dol_dgd_ring_edges_f32", X.data_ptr(), ldx, Y.data_ptr(), ldy, n, P, halo_prev.data_ptr(),
+                 halo_next.data_ptr(), w_prev.data_ptr(), w_next.data_ptr(), target.data_ptr(), ldt,
+                 _ptr(mom) if ldm else None, ldm, OBJECTIVES[objective], int(steps), float(lr), float(momentum),
+                 int(bool(first_step)), _stream(X))
     return Y
 
 

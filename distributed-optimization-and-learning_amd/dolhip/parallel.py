@@ -50,10 +50,14 @@ class ShardedRing:
     """
 
     def __init__(self, n_agents: int, P: int, w_prev, w_next, device, ld: Optional[int] = None,
-                 group=None, alloc: bool = True, mix_ring=None, dgd_ring=None):
-        # mix_ring / dgd_ring: kernel entries (default: the HIP ops); tests inject CPU checkers
+                 group=None, alloc: bool = True, mix_ring=None, dgd_ring=None, mix_edges=None, dgd_edges=None):
+        # mix_ring / dgd_ring / *_edges: kernel entries (default: the HIP ops); tests
+        # inject CPU checkers.  The boundary rows go in ONE launch (dol_*_ring_edges_f32);
+        # with an injected mix and no injected edge entry they go through the mix, one row each.
         self._mix = mix_ring if mix_ring is not None else ops.mix_ring
         self._dgd = dgd_ring if dgd_ring is not None else ops.dgd_ring
+        self._mix_edges = mix_edges if mix_edges is not None else (ops.mix_ring_edges if mix_ring is None else None)
+        self._dgd_edges = dgd_edges if dgd_edges is not None else (ops.dgd_ring_edges if dgd_ring is None else None)
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
@@ -131,10 +135,13 @@ class ShardedRing:
                     ev[1].record()
             self._finish_exchange(reqs)
             # boundary rows 0 and n-1
-            self._mix(x[0:1], y[0:1], self.w_prev[0:1], self.w_next[0:1], halo_prev=self.halo_prev,
-                      halo_next=x[1], P=P, n_rows=1)
-            self._mix(x[n - 1:n], y[n - 1:n], self.w_prev[n - 1:n], self.w_next[n - 1:n],
-                      halo_prev=x[n - 2], halo_next=self.halo_next, P=P, n_rows=1)
+            if self._mix_edges is not None:
+                self._mix_edges(x, y, self.w_prev, self.w_next, self.halo_prev, self.halo_next, P=P, n_rows=n)
+            else:
+                self._mix(x[0:1], y[0:1], self.w_prev[0:1], self.w_next[0:1], halo_prev=self.halo_prev,
+                          halo_next=x[1], P=P, n_rows=1)
+                self._mix(x[n - 1:n], y[n - 1:n], self.w_prev[n - 1:n], self.w_next[n - 1:n],
+                          halo_prev=x[n - 2], halo_next=self.halo_next, P=P, n_rows=1)
         if own:
             self.x, self.y = self.y, self.x
 
@@ -158,10 +165,14 @@ class ShardedRing:
                 if ev:
                     ev[1].record()
             self._finish_exchange(reqs)
-            self._dgd(x[0:1], y[0:1], self.w_prev[0:1], self.w_next[0:1], target[0:1], mom=m(0, 1),
-                      halo_prev=self.halo_prev, halo_next=x[1], P=P, n_rows=1, **kw)
-            self._dgd(x[n - 1:n], y[n - 1:n], self.w_prev[n - 1:n], self.w_next[n - 1:n], target[n - 1:n],
-                      mom=m(n - 1, n), halo_prev=x[n - 2], halo_next=self.halo_next, P=P, n_rows=1, **kw)
+            if self._dgd_edges is not None:
+                self._dgd_edges(x, y, self.w_prev, self.w_next, target, self.halo_prev, self.halo_next, mom=mom,
+                                P=P, n_rows=n, **kw)
+            else:
+                self._dgd(x[0:1], y[0:1], self.w_prev[0:1], self.w_next[0:1], target[0:1], mom=m(0, 1),
+                          halo_prev=self.halo_prev, halo_next=x[1], P=P, n_rows=1, **kw)
+                self._dgd(x[n - 1:n], y[n - 1:n], self.w_prev[n - 1:n], self.w_next[n - 1:n], target[n - 1:n],
+                          mom=m(n - 1, n), halo_prev=x[n - 2], halo_next=self.halo_next, P=P, n_rows=1, **kw)
         self.x, self.y = self.y, self.x
 
 
@@ -190,20 +201,27 @@ class ColumnSharded:
         self.Pl = self.c1 - self.c0
         self.device = torch.device(device)
         self.ld = row_stride(max(self.Pl, 1))
+        self._injected = (apply, apply_dgd)  # kept across set_plan (the tests' CPU checkers)
         self._apply = apply if apply is not None else plan.apply
         self._apply_dgd = apply_dgd if apply_dgd is not None else plan.apply_dgd
         if alloc:
             self.x = torch.empty(self.N, self.ld, dtype=torch.float32, device=self.device)
             self.y = torch.empty_like(self.x)
 
-    def set_plan(self, plan) -> None:
+    def set_plan(self, plan, apply=None, apply_dgd=None) -> None:
         """A new W for the next rounds (time-varying graphs, BASELINE config 5:
-        every rank draws the same W from the round's seed); same agent count."""
+        every rank draws the same W from the round's seed); same agent count.
+        Entries injected at construction (or passed here) stay in use; the
+        others follow the new plan's HIP ops."""
         if (plan.n_rows, plan.n_cols) != (self.N, self.plan.n_cols):
             raise ValueError("set_plan: the new W must have the same shape")
         self.plan = plan
-        self._apply = plan.apply
-        self._apply_dgd = plan.apply_dgd
+        if apply is not None or apply_dgd is not None:
+            self._injected = (apply if apply is not None else self._injected[0],
+                              apply_dgd if apply_dgd is not None else self._injected[1])
+        inj_apply, inj_dgd = self._injected
+        self._apply = inj_apply if inj_apply is not None else plan.apply
+        self._apply_dgd = inj_dgd if inj_dgd is not None else plan.apply_dgd
 
     def local_cols(self, full: torch.Tensor) -> torch.Tensor:
         """This rank's column block of a full [N, >=P] matrix."""

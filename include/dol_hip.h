@@ -83,8 +83,10 @@ int dol_mix_csr_pm_f32(const float* XT, int64_t ldx, int32_t x_rows, float* YT, 
  * dol_csr_slab_pack (rows in groups of DOL_SLAB_ROWS; for group g and chunk k
  * the entries of the group's rows with columns in the chunk are contiguous):
  *   ent  int32 [dol_csr_slab_ent_len(nnz, n_rows, x_rows)]: (LDS byte offset,
- *        weight bits) entries; every (row, chunk) segment padded to an even
- *        number of entries with a (0, 0) entry
+ *        weight bits) entries stored in pairs as (offset 0, offset 1, weight 0,
+ *        weight 1); every (row, chunk) segment padded to an even number of
+ *        entries with a (65536, 0) entry, which the kernel reads from a zero
+ *        piece in LDS (its +0 product leaves every sum's bits unchanged)
  *   hdr  int32 [dol_csr_slab_hdr_len(n_rows, x_rows)]: hdr[g][k][i] = ent
  *        index of row g*DOL_SLAB_ROWS+i's first entry in chunk k (i <= ROWS;
  *        even), bit 0 set when that segment ends in a pad entry
@@ -137,6 +139,17 @@ int dol_mix_ring_f32(const float* X, int64_t ldx, float* Y, int64_t ldy,
                      const float* halo_prev, const float* halo_next,
                      const float* w_prev, const float* w_next,
                      hipStream_t s);
+/*
+ * Only the two BOUNDARY rows (0 and n_rows - 1) of dol_mix_ring_f32 with halos,
+ * in one launch: the second half of a sharded ring round (the interior rows
+ * 1..n-2 are mixed while the halo rows travel between ranks, the reference's
+ * neighbour read DIST/simulators.py:96 become RCCL send/recv).  Same
+ * arithmetic as dol_mix_ring_f32; n_rows == 1 mixes its one row from both
+ * halos.  halo_prev / halo_next must be non-NULL.
+ */
+int dol_mix_ring_edges_f32(const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t n_rows, int64_t P,
+                           const float* halo_prev, const float* halo_next, const float* w_prev,
+                           const float* w_next, hipStream_t s);
 
 /*
  * `steps` synchronous ring rounds in ONE pass over HBM (temporal blocking):
@@ -216,6 +229,11 @@ int dol_dgd_csr_f32(const float* X, int64_t ldx, int32_t x_rows, float* Y, int64
                     const int32_t* rowptr, const int32_t* col, const float* val, const float* target, int64_t ldt,
                     float* mom, int64_t ldm, int32_t objective, int32_t local_steps, float lr, float momentum,
                     int first_step, hipStream_t s);
+/* the boundary rows of dol_dgd_ring_f32 in one launch (see dol_mix_ring_edges_f32) */
+int dol_dgd_ring_edges_f32(const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t n_rows, int64_t P,
+                           const float* halo_prev, const float* halo_next, const float* w_prev, const float* w_next,
+                           const float* target, int64_t ldt, float* mom, int64_t ldm, int32_t objective,
+                           int32_t local_steps, float lr, float momentum, int first_step, hipStream_t s);
 /*
  * dol_dgd_csr_f32 on the parameter-major bank (XT, YT as dol_mix_csr_pm_f32;
  * TT [P][ldt] the targets and MT [P][ldm] the momentum, transposed the same

@@ -384,3 +384,32 @@ def test_fedadmm_server_records_primal_dual_metrics(gpu):
     # round 0: alpha = rho (w - theta) from zero duals, so ||alpha||^2 = rho^2 ||w - theta||^2 (fp32 rounding)
     r0 = s.metrics[0]
     assert r0["dual_sq"] == pytest.approx(args.rho ** 2 * r0["primal_resid_sq"], rel=1e-5)
+
+
+def test_batched_momentum_paths_record_started_rows(gpu, tmp_path):
+    """The batched paths (AgentBank.local_step on a row slice, BatchedMLP.step)
+    set the per-row 'momentum started' flags that checkpoints carry, so a
+    resumed per-row optimizer continues buf = mu*buf + g."""
+    from dolhip.bank import AgentBank
+    from dolhip.mlp import BatchedMLP, mlp_layout
+    a = AgentBank(6, 40, gpu)
+    a.rows()[:] = torch.randn(6, 40, device=gpu)
+    a.buffer("grad")[:, :40] = torch.randn(6, 40, device=gpu)
+    a.buffer("mom", zero=True)
+    a.local_step(lr=0.1, momentum=0.5, first_step=True, agents=slice(1, 4))
+    assert a.mom_started == [False, True, True, True, False, False]
+    p = str(tmp_path / "bank.safetensors")
+    a.save(p)
+    b = AgentBank(6, 40, gpu)
+    b.load(p)
+    assert b.mom_started == a.mom_started
+    bank = AgentBank(3, mlp_layout(8, 32, 3), gpu)
+    bank.buffer("x").normal_(0, 0.1)
+    mlp = BatchedMLP(bank, 8, 32, 3)
+    mlp.step(torch.randn(3, 5, 8, device=gpu), torch.randint(0, 3, (3, 5), device=gpu), lr=0.1, momentum=0.5,
+             first_step=True)
+    assert bank.mom_started == [True, True, True]
+    mlp0 = BatchedMLP(AgentBank(2, mlp_layout(8, 32, 3), gpu), 8, 32, 3)
+    mlp0.step(torch.randn(2, 5, 8, device=gpu), torch.randint(0, 3, (2, 5), device=gpu), lr=0.1, momentum=0.0,
+              first_step=True)
+    assert mlp0.bank.mom_started == [False, False]

@@ -714,3 +714,41 @@ def test_stream_copy_rows_is_a_copy(gpu):
     assert (Y[:, 4096:] == 3.0).all()
     with pytest.raises(ops.DolNativeError):
         ops.stream_copy_rows(X, Y, P=4095)
+
+
+@pytest.mark.parametrize("n,P,extra", [(1, 37, 0), (2, 1000, 0), (5, 4099, 3), (7, 4096, 1)])
+def test_ring_edges_match_oracle(n, P, extra, gpu):
+    """dol_mix_ring_edges_f32 / dol_dgd_ring_edges_f32 (the sharded round's two
+    boundary rows in one launch): rows 0 and n-1 bit-exact vs the oracle's ring
+    with halos, every other row untouched; f4 and scalar-tail paths."""
+    rng = np.random.default_rng(n * 31 + P)
+    X = rng.standard_normal((n, P)).astype(np.float32)
+    T = rng.standard_normal((n, P)).astype(np.float32)
+    M = rng.standard_normal((n, P)).astype(np.float32)
+    hp, hn = (rng.standard_normal(P).astype(np.float32) for _ in range(2))
+    X[0, :3] = [np.inf, -0.0, 1e-40]
+    wp, wn = rng.random(n).astype(np.float32), rng.random(n).astype(np.float32)
+    ld = P + extra
+
+    def dev(a, fill=float("nan")):
+        t = torch.full((a.shape[0], ld), fill, device=gpu)
+        t[:, :P] = torch.from_numpy(a).to(gpu)
+        return t
+    Xd, Yd, Td, Md = dev(X), dev(np.full((n, P), 5.0, np.float32)), dev(T), dev(M)
+    hpd, hnd = torch.from_numpy(hp).to(gpu), torch.from_numpy(hn).to(gpu)
+    wpd, wnd = torch.from_numpy(wp).to(gpu), torch.from_numpy(wn).to(gpu)
+    ops.mix_ring_edges(Xd, Yd, wpd, wnd, hpd, hnd, P=P, n_rows=n)
+    torch.cuda.synchronize()
+    want = oracle.mix_ring(X, wp, wn, hp, hn)
+    got = Yd[:, :P].cpu().numpy()
+    edges = [0, n - 1]
+    assert bits_equal(got[edges], want[edges])
+    assert (got[1:n - 1] == 5.0).all(), "interior rows touched"
+    Yd2 = dev(np.full((n, P), 5.0, np.float32))
+    ops.dgd_ring_edges(Xd, Yd2, wpd, wnd, Td, hpd, hnd, mom=Md, steps=2, lr=0.05, momentum=0.9, P=P, n_rows=n)
+    torch.cuda.synchronize()
+    wy, wm = oracle.dgd_local(want, T, M, "least_squares", 2, 0.05, 0.9, False)
+    assert bits_equal(Yd2[:, :P].cpu().numpy()[edges], wy[edges])
+    gm = Md[:, :P].cpu().numpy()
+    assert bits_equal(gm[edges], wm[edges])
+    assert bits_equal(gm[1:n - 1], M[1:n - 1]), "interior momentum touched"

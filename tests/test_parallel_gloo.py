@@ -35,6 +35,20 @@ def cpu_mix_ring(X, Y, w_prev, w_next, halo_prev=None, halo_next=None, P=None, n
     return Y
 
 
+def cpu_mix_ring_edges(X, Y, w_prev, w_next, halo_prev, halo_next, P=None, n_rows=None):
+    """CPU stand-in for dol_mix_ring_edges_f32: rows 0 and n-1 of the block."""
+    n = X.shape[0] if n_rows is None else n_rows
+    P = X.shape[1] if P is None else P
+    hp, hn = halo_prev[:P].numpy(), halo_next[:P].numpy()
+    nxt0 = X[1, :P].numpy() if n > 1 else hn
+    Y[0, :P] = torch.from_numpy(oracle.mix_ring(X[0:1, :P].numpy(), w_prev[0:1].numpy(), w_next[0:1].numpy(),
+                                                hp, nxt0))
+    if n > 1:
+        Y[n - 1, :P] = torch.from_numpy(oracle.mix_ring(X[n - 1:n, :P].numpy(), w_prev[n - 1:n].numpy(),
+                                                        w_next[n - 1:n].numpy(), X[n - 2, :P].numpy(), hn))
+    return Y
+
+
 def cpu_ordered_sum(W, order, acc_in=None, out=None, scale=1.0, P=None):
     if W is None or order.numel() == 0:
         res = acc_in[:P].numpy().astype(np.float32)
@@ -56,7 +70,8 @@ def _worker(rank, world, port, N, P, rounds, order, q):
         X = rng.standard_normal((N, P)).astype(np.float32)
         wp = rng.random(N).astype(np.float32)
         wn = rng.random(N).astype(np.float32)
-        ring = parallel.ShardedRing(N, P, wp, wn, "cpu", ld=P + 3, mix_ring=cpu_mix_ring)
+        ring = parallel.ShardedRing(N, P, wp, wn, "cpu", ld=P + 3, mix_ring=cpu_mix_ring,
+                                    mix_edges=cpu_mix_ring_edges if rank % 2 else None)
         ring.x[:, :P] = torch.from_numpy(X[ring.lo:ring.hi])
         for _ in range(rounds):
             ring.step()
@@ -250,3 +265,23 @@ def test_column_sharded_set_plan_swaps_the_mix():
     assert calls == ["a", "b", "b-dgd"]
     with pytest.raises(ValueError):
         sh.set_plan(plan_of("c", n=7, m=7))
+
+
+def test_column_sharded_set_plan_keeps_injected_entries():
+    """Entries injected at construction (the CPU-checker hook) survive set_plan
+    (ADVICE r02): only un-injected entries follow the new plan."""
+    from types import SimpleNamespace
+    calls = []
+
+    def plan_of(tag):
+        return SimpleNamespace(n_rows=6, n_cols=6, apply=lambda x, y, P=None: calls.append(tag),
+                               apply_dgd=lambda *a, **k: calls.append(tag + "-dgd"))
+    sh = parallel.ColumnSharded(plan_of("a"), 10, "cpu", apply=lambda x, y, P=None: calls.append("checker"))
+    sh.step()
+    sh.set_plan(plan_of("b"))
+    sh.step()
+    sh.dgd_step(torch.zeros(6, sh.ld))
+    sh.set_plan(plan_of("c"), apply_dgd=lambda *a, **k: calls.append("dgd-checker"))
+    sh.dgd_step(torch.zeros(6, sh.ld))
+    sh.step()
+    assert calls == ["checker", "checker", "b-dgd", "dgd-checker", "checker"]

@@ -103,9 +103,11 @@ def test_slab_rectangular_and_low_degree_rows(gpu):
 def slab_pack_host(csr, x_rows):
     """Host restatement of dol_csr_slab_pack: rows in groups of SLAB_ROWS; for
     group g, chunk k the rows' chunk-k entries contiguous in (row, column)
-    order, each row's segment padded to an even length with a (0, 0) entry;
-    entry = (LDS byte offset (col % 64) * 1024, weight bits); header word =
-    segment start | (1 if padded)."""
+    order, each row's segment padded to an even length with a pad entry (offset
+    SLAB_ZERO_OFFSET = the stage's zero piece, weight 0); entry = (LDS byte
+    offset (col % 64) * 1024, weight bits); entries stored in PAIRS as (offset
+    0, offset 1, weight 0, weight 1); header word = segment start | (1 if
+    padded).  Returns (hdr, entries as an [n, 2] (offset, weight) array)."""
     R, C = ops.SLAB_ROWS, ops.SLAB_CHUNK
     nk = -(-x_rows // C)
     n_rg = -(-csr.n_rows // R)
@@ -124,9 +126,12 @@ def slab_pack_host(csr, x_rows):
                 for c, v in zip(cols[sel], vals[sel]):
                     ent.append(((int(c) % C) * 1024, int(np.float32(v).view(np.int32))))
                 if sel.sum() % 2:
-                    ent.append((0, 0))
+                    ent.append((SLAB_ZERO_OFFSET, 0))
                     hdr[g, k, i] |= 1
     return hdr, np.array(ent, np.int64).reshape(-1, 2)
+
+
+SLAB_ZERO_OFFSET = 64 * 1024  # csr_slab.hip kZeroRel: the zero piece after each 64-KiB X stage
 
 
 @pytest.mark.parametrize("n,p", [(200, 0.2), (300, 0.05)])
@@ -136,7 +141,8 @@ def test_slab_pack_matches_host(n, p, gpu):
     hdr, ent = slab_pack_host(csr, n)
     got_h = plan.hdr[: hdr.size].cpu().numpy().reshape(hdr.shape)
     assert np.array_equal(got_h, hdr)
-    got_e = plan.ent[: 2 * len(ent)].cpu().numpy().reshape(-1, 2)
+    pairs = plan.ent[: 2 * len(ent)].cpu().numpy().reshape(-1, 4)  # (off0, off1, w0, w1)
+    got_e = np.stack([pairs[:, [0, 1]].reshape(-1), pairs[:, [2, 3]].reshape(-1)], axis=1)
     assert np.array_equal(got_e, ent)
 
 
@@ -165,7 +171,12 @@ def test_from_dense_csr_plan_reuse_and_mix(gpu):
     plan = None
     for rnd in range(2):
         W = G.erdos_renyi_stochastic_hip(n, 0.1, seed=1000 + rnd, device=gpu)
+        prev = plan
         plan = G.MixingPlan.from_dense(W, dense_kernel="csr", reuse=plan)
+        if prev is not None:  # the lender is retired: its buffers now hold this round's W
+            assert prev.kind == "stale"
+            with pytest.raises(RuntimeError, match="lent its buffers"):
+                prev.apply(Xd, Yd, P=P)
         plan.apply(Xd, Yd, P=P)
         torch.cuda.synchronize()
         host = G.csr_from_dense(W.cpu())

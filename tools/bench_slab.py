@@ -51,14 +51,14 @@ def main():
         X = torch.empty(N, ld, device=dev).normal_(generator=g)
         Y = torch.empty_like(X)
         W = G.erdos_renyi_stochastic_hip(N, a.p, seed=2028, device=dev)
-        plan = G.MixingPlan.from_dense(W, dense_kernel="csr")
-        nnz = int(plan.rowptr[-1].item())
-        state = {"plan": plan}
+        state = {"plan": G.MixingPlan.from_dense(W, dense_kernel="csr")}
 
-        def draw_csr():
+        def draw_csr():  # retires the previous plan (its buffers are reused)
             state["plan"] = G.MixingPlan.from_dense(W, dense_kernel="csr", reuse=state["plan"])
-        base = {"agents": N, "params": P, "p_edge": a.p, "nnz": nnz, "mean_degree": nnz / N}
         t_build = timed(draw_csr, a.reps)
+        plan = state["plan"]
+        nnz = int(plan.rowptr[-1].item())
+        base = {"agents": N, "params": P, "p_edge": a.p, "nnz": nnz, "mean_degree": nnz / N}
         for path in a.paths:
             if path == "slab":
                 ms = timed(lambda: plan.apply(X, Y, P=P), a.reps)
