@@ -168,6 +168,49 @@ def cpu_baseline(sizes, P: int, seconds: float, full_agents: int):
     }
 
 
+def cpu_secondaries(P: int, full_agents: int, admm_sizes=(64, 256), cfg5_sizes=(128, 256), cfg5_agents: int = 1024):
+    """CPU legs beside the secondaries (reference-structured torch-CPU code in
+    oracle/ref_cpu.py, same threads as cpu_baseline):
+      * FedADMM: FedAdmm_Client.update_weights (autograd least-squares loss +
+        the ADMM term + SGD momentum, 10 local steps) + update_duals + the
+        server's deepcopy + average_weights (DEC/clients.py:36-53,125-144,
+        DEC/servers.py:42-48) over n clients x P; the per-client cost does not
+        depend on n, so `value` = the largest n's rate x n / full_agents;
+      * config 5: every agent's 784-128-10 MLP step (nn.Module, CrossEntropyLoss,
+        SGD momentum, batch 32; DIST/clients.py:34-59) + the consensus round
+        with a new ER p = 0.1 W (Neighbors scan + consensus + load_state_dict);
+        Neighbors and consensus grow as n^2, so `value` = the largest n's rate x
+        (n / cfg5_agents)^2 (their share; the linear local steps make it
+        conservative for the GPU's ratio)."""
+    from oracle import ref_cpu
+    threads = torch.get_num_threads()
+    adm = {}
+    for n in admm_sizes:
+        _log(f"cpu FedADMM: {n} clients x {P}")
+        r, sec = ref_cpu.time_admm_rounds(n, P, warmup=n <= 64)
+        adm[n] = {"rounds": r, "seconds": sec, "rounds_per_s": r / sec, "ms_per_client": sec / r / n * 1e3}
+    big = max(admm_sizes)
+    c5 = {}
+    for n in cfg5_sizes:
+        _log(f"cpu config 5: {n} agents")
+        r, sec = ref_cpu.time_config5_rounds(n, warmup=n <= 128)
+        c5[n] = {"rounds": r, "seconds": sec, "rounds_per_s": r / sec}
+    b5 = max(cfg5_sizes)
+    return {
+        "fedadmm": {"value": adm[big]["rounds_per_s"] * big / full_agents, "unit": "rounds/s", "cores": threads,
+                    "kind": "port", "per_clients": adm,
+                    "sample": f"reference-structured torch-CPU FedADMM round (oracle/ref_cpu.py AdmmClient + "
+                              f"average_weights), 10 local steps, n in {list(admm_sizes)} x {P}; value = the n={big} "
+                              f"rate x {big}/{full_agents} (per client, linear)"},
+        "config5": {"value": c5[b5]["rounds_per_s"] * (b5 / cfg5_agents) ** 2, "unit": "rounds/s", "cores": threads,
+                    "kind": "port", "per_agents": c5,
+                    "sample": f"reference-structured torch-CPU config-5 round (oracle/ref_cpu.py "
+                              f"time_config5_rounds: per-agent nn.Module MLP step + ER W Neighbors/consensus), n in "
+                              f"{list(cfg5_sizes)}; value = the n={b5} rate x ({b5}/{cfg5_agents})^2 (the O(n^2) "
+                              f"scan and consensus)"},
+    }
+
+
 def primal_dual_round(N: int, P: int, world: int, rank: int, device, steps: int, local_steps: int = 10):
     """Secondary measurement (BASELINE config 4, primal/dual side): one FedADMM
     round of dolhip.synthetic.SeparableADMM on least squares over ALL N agents
@@ -486,6 +529,9 @@ def main():
     rr_pm = None
     if world == 1 and not args.no_primal_dual and N <= 8192:
         rr_pm = random_regular_pm_round(device, ring.x, ring.y, N, P)
+        # the same-box yardstick: the headline ring kernel moves the same bytes
+        rr_pm["ring_kernel_ms_same_box"] = kern_ms
+        rr_pm["ring_over_pm"] = kern_ms / rr_pm["ms_per_round"]
     _log("random-regular pm done")
     calib = None
     if not args.no_copy:
@@ -523,6 +569,14 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu:
             cpu = cpu_baseline(args.cpu_agents, P, args.cpu_seconds, N)
+            if not args.no_primal_dual:
+                sec = cpu_secondaries(P, N)
+                if pd_round is not None:
+                    pd_round["cpu_baseline"] = sec["fedadmm"]
+                    pd_round["vs_cpu"] = pd_round["rounds_per_s"] / sec["fedadmm"]["value"]
+                if cfg5 is not None:
+                    cfg5["cpu_baseline"] = sec["config5"]
+                    cfg5["vs_cpu"] = cfg5["rounds_per_s"] / sec["config5"]["value"]
         value = K / elapsed
         out = {
             "metric": METRIC,

@@ -186,3 +186,32 @@ def test_separable_admm_rejects_bad_orders():
     for bad in ([4], [-1], [1, 1], []):
         with pytest.raises(ValueError):
             s.round(order=bad)
+
+
+def test_ref_cpu_admm_baseline_matches_oracle():
+    """bench.py's CPU FedADMM leg (oracle/ref_cpu.py, reference-structured torch
+    code) computes the same round as the oracle the kernels are pinned to, so
+    the GPU/CPU ratio compares like with like."""
+    import copy
+    from oracle import ref_cpu
+    n, P, steps, rho, lr, mu = 5, 37, 3, 0.1, 0.1, 0.5
+    g = torch.Generator().manual_seed(4)
+    T = [torch.randn(P, generator=g) for _ in range(n)]
+    clients = [ref_cpu.AdmmClient(t, rho, lr, mu, steps) for t in T]
+    theta = {"w": torch.randn(P, generator=g)}
+    w0 = np.zeros((n, P), np.float32)
+    b0 = np.zeros((n, P), np.float32)
+    a0 = np.zeros((n, P), np.float32)
+    Tn = np.stack([t.numpy() for t in T])
+    th = theta["w"].numpy().copy()
+    first = np.ones(n, np.int32)
+    order = np.arange(n, dtype=np.int32)
+    for _ in range(2):
+        local = [copy.deepcopy(c.update_weights(theta)) for c in clients]
+        theta = ref_cpu.average_weights(local)
+        w0, b0, a0, _, _ = oracle.admm_ls_round(w0, b0, a0, Tn, th, order, first, rho, lr, mu, steps)
+        th = oracle.ordered_mean(w0, order)
+        first = np.zeros(n, np.int32)
+        assert bits_equal(np.stack([c.model.w.detach().numpy() for c in clients]), w0)
+        assert bits_equal(np.stack([c.alpha["w"].numpy() for c in clients]), a0)
+        assert bits_equal(theta["w"].numpy(), th)

@@ -50,7 +50,7 @@ def _worker(rank, world, port, N, P, rounds, order, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,N", [(2, 64), (3, 50)])
+@pytest.mark.parametrize("world,N", [(2, 64), (3, 50), (8, 64)])
 def test_sharded_ring_real_kernels_on_one_gpu(world, N):
     import oracle
     P, rounds = 4096 + 12, 3
@@ -287,3 +287,67 @@ def test_sharded_dgd_ring_real_kernels_on_one_gpu(world, N):
         X, M = oracle.dgd_local(oracle.mix_ring(X, wp, wn), T, M, "least_squares", 2, 0.1, 0.5, k == 0)
     assert oracle.bits_equal(np.concatenate([r[1] for r in res]), X)
     assert oracle.bits_equal(np.concatenate([r[2] for r in res]), M)
+
+
+def _admm_worker(rank, world, port, N, P, rounds, mean, kw, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "distributed-optimization-and-learning_amd"))
+    from dolhip.synthetic import SeparableADMM
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        s = SeparableADMM(N, P, device=torch.device("cuda:0"), mean=mean, **kw)
+        for _ in range(rounds):
+            s.round()
+        torch.cuda.synchronize()
+        q.put((rank, s.w[:s.n, :P].cpu().numpy(), s.alpha[:s.n, :P].cpu().numpy(), s.mom[:s.n, :P].cpu().numpy(),
+               s.theta[:P].cpu().numpy(), [h["primal_resid_sq"] for h in s.history]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,mean", [(8, "exact"), (8, "fast"), (3, "exact")])
+def test_sharded_admm_real_kernels_on_one_gpu(world, mean, gpu):
+    """Config 4's FedADMM (SeparableADMM: dol_admm_ls_round_f32 per rank's agent
+    block + the ordered chain mean or local sum + all_reduce) at world 8 with the
+    real kernels, against one process on the same GPU: w / alpha / momentum of
+    every agent and theta bit-identical ("exact"; DEC/servers.py:42-48's order),
+    theta within fp32 rounding of the all_reduce sum ("fast").  Reference:
+    DEC/clients.py:36-53,125-144, DEC/servers.py:50-81."""
+    from dolhip.synthetic import SeparableADMM
+    N, P, rounds = 67, 3000 + 7, 3
+    kw = dict(rho=0.1, lr=0.1, momentum=0.5, local_steps=4, frac=0.7, seed=11)
+    ref = SeparableADMM(N, P, device=gpu, mean="exact", **kw)
+    for _ in range(rounds):
+        ref.round()
+    torch.cuda.synchronize()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_admm_worker, args=(r, world, port, N, P, rounds, mean, kw, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    import oracle
+    w = np.concatenate([r[1] for r in res])
+    a = np.concatenate([r[2] for r in res])
+    b = np.concatenate([r[3] for r in res])
+    for got, want in ((w, ref.w), (a, ref.alpha), (b, ref.mom)):
+        want = want[:N, :P].cpu().numpy()
+        if mean == "exact":
+            assert oracle.bits_equal(got, want)
+        else:  # theta differs by the all_reduce's rounding from round 2 on
+            np.testing.assert_allclose(got, want, rtol=1e-4, atol=1e-5)
+    hist = [h["primal_resid_sq"] for h in ref.history]
+    th = ref.theta[:P].cpu().numpy()
+    for r in res:
+        if mean == "exact":
+            assert oracle.bits_equal(r[4], th)
+            np.testing.assert_allclose(r[5], hist, rtol=1e-9)
+        else:
+            np.testing.assert_allclose(r[4], th, rtol=1e-5, atol=1e-6)
