@@ -81,7 +81,10 @@ static_assert(kLds <= 160 * 1024, "LDS budget");
 #define DOL_LPTR(p) ((__attribute__((address_space(3))) void*)(p))
 
 struct alignas(16) I4 {
-  int32_t x, y, z, w;  // a PAIR of entries: (offset 0, offset 1, weight bits 0, weight bits 1)
+  // a PAIR of entries: (weight bits 0, offset 0, weight bits 1, offset 1) -- each
+  // weight in an even register of the loaded quad, so v_pk_mul_f32 broadcasts it
+  // straight from there (op_sel_hi), no copy into an aligned pair
+  int32_t w0, o0, w1, o1;
 };
 
 // LDS-DMA of 16 B per lane (1 KiB per wave) from `gptr` to the wave-uniform LDS
@@ -106,7 +109,9 @@ __device__ __forceinline__ uint32_t piece_addr(uint32_t o, uint32_t lb) { return
 
 // PROBE (diagnostics, DOL_SLAB_PROBE; results meaningless except 0): 1 = staging
 // only (no gathers), 2 = no X staging (index blocks and gathers only), 3 = no
-// workgroup barrier per chunk (waves drift; reads race the DMA).
+// workgroup barrier per chunk (waves drift; reads race the DMA), 4 = no index
+// reads inside a row (every step reuses the row's first two pairs), 5 = the
+// products' multiplies dropped (acc += x: half the VALU).
 // Each row walks its chunk segment in groups of 4 / 2 / 1 entries: the index
 // pairs by uniform ds_read_b128 (segments are padded to even lengths, so two
 // entries share one 16-B LDS read: 2 LDS cycles per entry; ds_read2_b64 took
@@ -157,6 +162,7 @@ __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
     it.H = hdr + int64_t(it.rg) * nk * (kRows + 1);
     return true;
   };
+  const int32_t* perm = hdr + int64_t(n_rg) * nk * (kRows + 1);  // slot -> output row (dol_csr_slab_pack)
   int64_t t = blockIdx.x;
   Item cur, nxt;
   if (!item_at(t, cur)) return;
@@ -168,13 +174,28 @@ __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
   int hv = 0;                                 // header lanes, see issue()
   // stage chunk k of item `it` into buffer `buf`; `after` = the item whose chunk 0
   // follows it when k is the last chunk (nullptr: none)
+  // LDS byte address of the dynamic LDS (hoisted: the generic -> local cast
+  // costs a null check per use)
+  const uint32_t lds_base = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(DOL_LPTR(lds)));
   auto issue = [&](const Item& it, int k, int buf, const Item* after) {
-    uint8_t* dst = lds + buf * kStage;
+    if constexpr (PROBE != 2) {
+      // this wave's kPerWave agent pieces of the chunk: one 64-bit product per
+      // chunk, then a row stride per piece (agents past x_rows: the last row
+      // again, never referenced)
+      const int a0w = k * kChunk + wave * kPerWave;
+      const uint32_t la = lds_base + uint32_t(buf * kStage + wave * kPerWave * 1024);
+      if (a0w + kPerWave <= x_rows) {
+        const float* src = it.xsrc + int64_t(a0w) * ldx;
 #pragma unroll
-    for (int i = 0; i < kPerWave && PROBE != 2; ++i) {
-      const int al = wave * kPerWave + i;
-      const int a = min(k * kChunk + al, x_rows - 1);  // agents past x_rows: never referenced
-      dma16(it.xsrc + int64_t(a) * ldx, dst + al * 1024);
+        for (int i = 0; i < kPerWave; ++i)
+          asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(src + i * ldx), "{m0}"(la + i * 1024) : "memory");
+      } else {
+#pragma unroll
+        for (int i = 0; i < kPerWave; ++i) {
+          const float* src = it.xsrc + int64_t(min(a0w + i, x_rows - 1)) * ldx;
+          asm volatile("global_load_lds_dwordx4 %0, off" ::"v"(src), "{m0}"(la + i * 1024) : "memory");
+        }
+      }
     }
     // the chunk's index block (16-B aligned start, whole 1 KiB pieces; ent is padded)
     const int64_t a0 = int64_t(blk0 & ~1) * 8;  // even: 16-B aligned
@@ -222,56 +243,81 @@ __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
 #pragma unroll
         for (int r = 0; r < kRW; ++r)
           for (int e = bnd[r]; e < bnd[r + 1]; ++e) {
-            const int64_t q = int64_t(e >> 1) * 4 + (e & 1);
-            acc[r] = fmac(acc[r], __int_as_float(ent[q + 2]), gather(ent[q]));
+            const int64_t q = int64_t(e >> 1) * 4 + 2 * (e & 1);  // (weight, offset)
+            acc[r] = fmac(acc[r], __int_as_float(ent[q]), gather(ent[q + 1]));
           }
         continue;
       }
       // This wave's rows' segments are one contiguous run of entry pairs in the
       // block (row order; every segment an even number of entries, pads
-      // included).  The wave walks it with the next two pairs always in flight:
-      // one uniform ds_read_b128 per pair (2 LDS cycles per entry), read while
-      // the current pairs' gathers are outstanding, so each step waits on one
-      // LDS round trip (the gathers) instead of two.  The run may be read up to
-      // kAhead bytes past its end (inside the stage: `fits` leaves the room).
-      uint32_t ip = uint32_t(kIdxBase + (g & 1) * kIdxBytes + (bnd[0] - e0) * 8);
+      // included).  Row r's first two pairs are read while row r - 1 is being
+      // summed (fa / fb), so a row never starts on an index round trip; inside
+      // a row the pairs go two at a time with the next two pairs' index read
+      // behind the current gathers, the loop unrolled twice so the prefetched
+      // index lands in the registers the next step reads (no copies).  Reads
+      // run at most kAhead bytes past the wave's run (inside the stage:
+      // `fits` leaves the room).
+      const uint32_t ibase = uint32_t(kIdxBase + (g & 1) * kIdxBytes) - uint32_t(e0) * 8;
       auto pair_at = [&](uint32_t a) { return *static_cast<const I4*>(__builtin_assume_aligned(lds + a, 16)); };
-      I4 qa = pair_at(ip), qb = pair_at(ip + 16);
-      ip += 32;
+      auto step2 = [&](f4 a, const I4& p, const I4& q) {  // four entries: p's pair, then q's
+        const f4 x0 = gather(p.o0), x1 = gather(p.o1), x2 = gather(q.o0), x3 = gather(q.o1);
+        if constexpr (PROBE == 5) return a + x0 + x1 + x2 + x3;
+        a = fmac(a, __int_as_float(p.w0), x0);
+        a = fmac(a, __int_as_float(p.w1), x1);
+        a = fmac(a, __int_as_float(q.w0), x2);
+        return fmac(a, __int_as_float(q.w1), x3);
+      };
+      I4 fa = pair_at(ibase + uint32_t(bnd[0]) * 8), fb = pair_at(ibase + uint32_t(bnd[0]) * 8 + 16);
 #pragma unroll
       for (int r = 0; r < kRW; ++r) {
         int np = (bnd[r + 1] - bnd[r]) >> 1;  // pairs of row r in this chunk
-        f4 a = acc[r];
-        for (; np >= 2; np -= 2) {
-          const f4 x0 = gather(qa.x), x1 = gather(qa.y), x2 = gather(qb.x), x3 = gather(qb.y);
-          const I4 na = pair_at(ip), nb = pair_at(ip + 16);
-          ip += 32;
-          a = fmac(a, __int_as_float(qa.z), x0);
-          a = fmac(a, __int_as_float(qa.w), x1);
-          a = fmac(a, __int_as_float(qb.z), x2);
-          a = fmac(a, __int_as_float(qb.w), x3);
-          qa = na;
-          qb = nb;
+        I4 qa = fa, qb = fb;
+        if (r + 1 < kRW) {  // the next row's first two pairs
+          const uint32_t nx = ibase + uint32_t(bnd[r + 1]) * 8;
+          fa = pair_at(nx);
+          fb = pair_at(nx + 16);
         }
-        if (np) {
-          const f4 x0 = gather(qa.x), x1 = gather(qa.y);
-          const I4 nb = pair_at(ip);
-          ip += 16;
-          a = fmac(a, __int_as_float(qa.z), x0);
-          a = fmac(a, __int_as_float(qa.w), x1);
-          qa = qb;
-          qb = nb;
+        uint32_t ip = ibase + uint32_t(bnd[r]) * 8 + 32;  // the pair after qb
+        f4 a = acc[r];
+        while (np >= 4) {
+          const I4 na = PROBE == 4 ? qb : pair_at(ip), nb = PROBE == 4 ? qa : pair_at(ip + 16);
+          a = step2(a, qa, qb);
+          // qa / qb are free once this step's products are summed: reload them
+          // only then, into the same registers (a hoisted reload needs fresh
+          // registers and a copy back at the loop end)
+          asm volatile("" : "+v"(a)::"memory");
+          if constexpr (PROBE != 4) {
+            qa = pair_at(ip + 32);
+            qb = pair_at(ip + 48);
+          }
+          ip += 64;
+          a = step2(a, na, nb);
+          asm volatile("" : "+v"(a)::"memory");
+          np -= 4;
+        }
+        if (np >= 2) {
+          I4 na;
+          if (np == 3) na = pair_at(ip);
+          a = step2(a, qa, qb);
+          if (np == 3) {
+            a = fmac(a, __int_as_float(na.w0), gather(na.o0));
+            a = fmac(a, __int_as_float(na.w1), gather(na.o1));
+          }
+        } else if (np == 1) {
+          a = fmac(a, __int_as_float(qa.w0), gather(qa.o0));
+          a = fmac(a, __int_as_float(qa.w1), gather(qa.o1));
         }
         acc[r] = a;
       }
     }
     const int64_t p = cur.p;
     if (p < P) {
-      const int grow0 = cur.rg * kRows + row0;
+      const int32_t* pr = perm + int64_t(cur.rg) * kRows + row0;
 #pragma unroll
       for (int r = 0; r < kRW; ++r) {
-        if (grow0 + r < n_rows) {
-          float* y = Y + int64_t(grow0 + r) * ldy + p;
+        const int row = pr[r];  // this wave's slot r holds output row `row` (-1: none)
+        if (row >= 0) {
+          float* y = Y + int64_t(row) * ldy + p;
           if (p + 4 <= P) {
             __builtin_nontemporal_store(acc[r], reinterpret_cast<f4*>(y));
           } else {
@@ -446,22 +492,120 @@ __global__ __launch_bounds__(1024) void slab_scan_kernel(int32_t* __restrict__ h
   }
 }
 
+// Row balancing (one wave per row group).  The mix kernel syncs its 16 waves
+// once per chunk, so a chunk costs the wave with the most entries in it; with
+// rows dealt to waves in index order the per-chunk maxima run ~22 % above the
+// mean at p = 0.1.  Greedy vector packing: rows by total entries (descending,
+// ties by index), each to the wave with < kRW rows whose chunk loads grow the
+// least in sum of squares, sum_k c_k (2 L_wk + c_k) (ties: lowest wave).  A
+// row's sum order is untouched (its entries keep their ascending-column
+// order), so the output bits are the same for any assignment.  In: hdr[g][k][i]
+// = padded entry count of row g R + i in chunk k (natural order).  Out: the
+// same counts in slot order (slot = wave * kRW + position), perm[g][slot] =
+// output row (-1: none), inv[g R + i] = slot.  nk > kBalMaxNk (x_rows > 32768)
+// or DOL_SLAB_BALANCE = 0: slots in row order.
+constexpr int kBalMaxNk = 512;
+__global__ __launch_bounds__(64) void slab_balance_kernel(int32_t* __restrict__ hdr, int n_rows, int nk,
+                                                          int32_t* __restrict__ perm, int32_t* __restrict__ inv,
+                                                          int balance) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t bl[];
+  int* L = reinterpret_cast<int*>(bl);                  // [kWaves][nk] wave loads
+  int* tot = L + kWaves * nk;                           // [kRows] row totals, then order
+  int* slot_of = tot + kRows;                           // [kRows]
+  uint8_t* c = reinterpret_cast<uint8_t*>(slot_of + kRows);  // [kRows][nk] counts (<= kChunk)
+  const int g = blockIdx.x, lane = threadIdx.x;
+  if (!balance) {  // slots in row order: the counts are already in slot order
+    for (int i = lane; i < kRows; i += 64) {
+      const int r = g * kRows + i;
+      perm[int64_t(g) * kRows + i] = r < n_rows ? r : -1;
+      if (r < n_rows) inv[r] = i;
+    }
+    return;
+  }
+  int32_t* H = hdr + int64_t(g) * nk * (kRows + 1);
+  for (int64_t j = lane; j < int64_t(kRows) * nk; j += 64) {
+    const int i = int(j / nk), k = int(j % nk);
+    c[j] = uint8_t(H[int64_t(k) * (kRows + 1) + i]);
+  }
+  for (int j = lane; j < kWaves * nk; j += 64) L[j] = 0;
+  __syncthreads();
+  {
+    for (int i = lane; i < kRows; i += 64) {
+      int t = 0;
+      for (int k = 0; k < nk; ++k) t += c[i * nk + k];
+      tot[i] = t;
+    }
+    __syncthreads();
+    int rk[2];
+    for (int h = 0; h < 2; ++h) {
+      const int i = lane + 64 * h, ti = tot[i];
+      int r = 0;
+      for (int j = 0; j < kRows; ++j) {
+        const int tj = tot[j];
+        r += (tj > ti) | ((tj == ti) & (j < i));
+      }
+      rk[h] = r;
+    }
+    __syncthreads();
+    tot[rk[0]] = lane;  // tot becomes order[]: rows by rank
+    tot[rk[1]] = lane + 64;
+    __syncthreads();
+    const int w = lane & (kWaves - 1), q = lane >> 4;  // this lane: wave w, chunks k = q mod 4
+    int filled = 0;                                    // rows dealt to wave w
+    for (int s = 0; s < kRows; ++s) {
+      const int i = tot[s];
+      const uint8_t* ci = c + i * nk;
+      int part = 0;
+      for (int k = q; k < nk; k += 4) {
+        const int ck = ci[k];
+        part += ck * (2 * L[w * nk + k] + ck);
+      }
+      part += __shfl_xor(part, 16);
+      part += __shfl_xor(part, 32);
+      int64_t key = filled < kRW ? (int64_t(part) << 4) | w : INT64_MAX;
+#pragma unroll
+      for (int o = 1; o < kWaves; o <<= 1) {
+        const int64_t other = __shfl_xor(key, o);
+        key = other < key ? other : key;
+      }
+      const int wb = int(key & (kWaves - 1));
+      if (w == wb) {
+        for (int k = q; k < nk; k += 4) L[w * nk + k] += ci[k];
+      }
+      if (lane == wb) slot_of[i] = wb * kRW + filled;
+      filled += (w == wb);
+      __syncthreads();
+    }
+  }
+  __syncthreads();
+  for (int i = lane; i < kRows; i += 64) {
+    const int r = g * kRows + i, sl = slot_of[i];
+    perm[int64_t(g) * kRows + sl] = r < n_rows ? r : -1;
+    if (r < n_rows) inv[r] = sl;
+  }
+  for (int64_t j = lane; j < int64_t(kRows) * nk; j += 64) {
+    const int i = int(j / nk), k = int(j % nk);
+    H[int64_t(k) * (kRows + 1) + slot_of[i]] = c[j];
+  }
+}
+
 // one wave per row: entries to their chunk-major slots as (LDS byte offset,
 // weight bits); then, per chunk with an odd count, a (0, 0) pad entry closes the
 // segment and bit 0 of the segment's header word is set
 __global__ __launch_bounds__(64) void slab_scatter_kernel(const int32_t* __restrict__ rowptr,
                                                           const int32_t* __restrict__ col,
                                                           const float* __restrict__ val, int nk,
+                                                          const int32_t* __restrict__ inv,
                                                           int32_t* __restrict__ hdr, int32_t* __restrict__ ent) {
-  const int r = blockIdx.x, g = r / kRows, i = r % kRows;
+  const int r = blockIdx.x, g = r / kRows, i = inv[r];
   const int e0 = rowptr[r], e1 = rowptr[r + 1];
   for (int e = e0 + int(threadIdx.x); e < e1; e += 64) {
     const int c = col[e], k = c / kChunk;
     const int first = lower_bound_col(col, e0, e1, k * kChunk);
     const int64_t dst = hdr[(int64_t(g) * nk + k) * (kRows + 1) + i] + (e - first);
-    const int64_t q = (dst >> 1) * 4 + (dst & 1);  // pair layout (off0, off1, w0, w1)
-    ent[q] = (c % kChunk) * (kCols * 4);
-    ent[q + 2] = __float_as_int(val[e]);
+    const int64_t q = (dst >> 1) * 4 + 2 * (dst & 1);  // pair layout (w0, off0, w1, off1)
+    ent[q] = __float_as_int(val[e]);
+    ent[q + 1] = (c % kChunk) * (kCols * 4);
   }
   __syncthreads();  // every header read above is done before the pad bits change them
   for (int k = int(threadIdx.x); k < nk; k += 64) {
@@ -470,9 +614,9 @@ __global__ __launch_bounds__(64) void slab_scatter_kernel(const int32_t* __restr
     if (n & 1) {
       int32_t* h = hdr + (int64_t(g) * nk + k) * (kRows + 1) + i;
       const int64_t pad = *h + n;  // odd: the second slot of the segment's last pair
-      const int64_t q = (pad >> 1) * 4 + 1;
-      ent[q] = kZeroRel;
-      ent[q + 2] = 0;
+      const int64_t q = (pad >> 1) * 4 + 2;  // (w1, off1) of the pair
+      ent[q] = 0;
+      ent[q + 1] = kZeroRel;
       *h |= 1;
     }
   }
@@ -485,7 +629,8 @@ inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 extern "C" int dol_csr_slab_nk(int32_t x_rows) { return x_rows <= 0 ? 0 : int((int64_t(x_rows) + kChunk - 1) / kChunk); }
 extern "C" int64_t dol_csr_slab_hdr_len(int32_t n_rows, int32_t x_rows) {
   if (n_rows <= 0 || x_rows <= 0) return 0;
-  return cdiv(n_rows, kRows) * dol_csr_slab_nk(x_rows) * (kRows + 1);
+  const int64_t n_rg = cdiv(n_rows, kRows);
+  return n_rg * dol_csr_slab_nk(x_rows) * (kRows + 1) + n_rg * kRows + n_rg * kRows;  // blocks, perm, inv
 }
 extern "C" int64_t dol_csr_slab_ent_len(int64_t nnz_cap, int32_t n_rows, int32_t x_rows) {
   if (nnz_cap < 0 || nnz_cap > dol::kMaxDim || n_rows < 0 || x_rows < 0) return 0;
@@ -533,24 +678,36 @@ extern "C" int dol_mix_csr_slab_f32(const float* X, int64_t ldx, int32_t x_rows,
   if (probe == 1) launch(csr_slab_kernel<1>);
   else if (probe == 2) launch(csr_slab_kernel<2>);
   else if (probe == 3) launch(csr_slab_kernel<3>);
+  else if (probe == 4) launch(csr_slab_kernel<4>);
+  else if (probe == 5) launch(csr_slab_kernel<5>);
   else launch(csr_slab_kernel<0>);
   return dol::check_launch("dol_mix_csr_slab_f32");
 }
 
 extern "C" int dol_csr_slab_pack(const int32_t* rowptr, const int32_t* col, const float* val, int32_t n_rows,
-                                 int32_t x_rows, int32_t* ent, int32_t* hdr, hipStream_t s) {
+                                 int32_t x_rows, int32_t balance, int32_t* ent, int32_t* hdr, hipStream_t s) {
   using dol::fail;
   if (n_rows < 0 || x_rows < 0) return fail(DOL_EINVAL, "dol_csr_slab_pack: negative size");
   if (n_rows == 0 || x_rows == 0) return DOL_OK;
   if (!rowptr || !ent || !hdr) return fail(DOL_EINVAL, "dol_csr_slab_pack: null pointer");
   const int nk = dol_csr_slab_nk(x_rows);
-  const int64_t len = dol_csr_slab_hdr_len(n_rows, x_rows);
+  const int64_t len = cdiv(n_rows, kRows) * nk * (kRows + 1);  // the header blocks
   if (cdiv(len, 256) >= (int64_t(1) << 31)) return fail(DOL_EINVAL, "dol_csr_slab_pack: too many chunk blocks");
   hipLaunchKernelGGL(slab_count_kernel, dim3(static_cast<unsigned>(cdiv(len, 256))), dim3(256), 0, s, rowptr, col,
                      n_rows, nk, len, hdr);
-  hipLaunchKernelGGL(slab_scan_kernel, dim3(1), dim3(1024), 0, s, hdr, len);
+  const int64_t n_rg = cdiv(n_rows, kRows);
+  const int64_t blocks = n_rg * nk * (kRows + 1);  // the header blocks; perm and inv follow
+  int32_t* perm = hdr + blocks;
+  int32_t* inv = perm + n_rg * kRows;
+  const int bal = balance && nk <= kBalMaxNk;  // beyond: slots in row order
+  const size_t bal_lds = bal ? size_t(kWaves) * nk * 4 + 2 * kRows * 4 + size_t(kRows) * nk : 16;
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(slab_balance_kernel),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(bal_lds));
+  hipLaunchKernelGGL(slab_balance_kernel, dim3(static_cast<unsigned>(n_rg)), dim3(64), bal_lds, s, hdr, n_rows, nk,
+                     perm, inv, bal);
+  hipLaunchKernelGGL(slab_scan_kernel, dim3(1), dim3(1024), 0, s, hdr, blocks);
   hipLaunchKernelGGL(slab_scatter_kernel, dim3(static_cast<unsigned>(n_rows)), dim3(64), 0, s, rowptr, col, val, nk,
-                     hdr, ent);
+                     inv, hdr, ent);
   return dol::check_launch("dol_csr_slab_pack");
 }
 

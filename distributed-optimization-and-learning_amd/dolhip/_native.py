@@ -71,7 +71,7 @@ SIGNATURES = {
     "dol_csr_slab_hdr_len": [_i32, _i32],
     "dol_csr_slab_ent_len": [_i64, _i32, _i32],
     "dol_mix_csr_slab_f32": [_ptr, _i64, _i32, _ptr, _i64, _i32, _i64, _ptr, _ptr, _ptr],
-    "dol_csr_slab_pack": [_ptr, _ptr, _ptr, _i32, _i32, _ptr, _ptr, _ptr],
+    "dol_csr_slab_pack": [_ptr, _ptr, _ptr, _i32, _i32, _i32, _ptr, _ptr, _ptr],
     "dol_dense_to_csr_f32": [_ptr, _i64, _i32, _i32, _ptr, _ptr, _ptr, _i64, _ptr],
 }
 _RESTYPES = {"dol_last_error": ctypes.c_char_p, "dol_admm_dual_workspace_bytes": ctypes.c_int64,

@@ -374,7 +374,7 @@ class MixingPlan:
             slab = csr.nnz >= self.SLAB_MIN_DEGREE * max(1, csr.n_rows)
         if self.kind == "csr" and slab and csr.n_rows > 0:
             from . import ops
-            self.ent, self.hdr = ops.csr_slab_pack(self.rowptr, self.col, self.val, self.n_cols)
+            self.ent, self.hdr = ops.csr_slab_pack(self.rowptr, self.col, self.val, self.n_cols, balance=True)
 
     @property
     def density(self) -> float:

@@ -127,13 +127,16 @@ SLAB_ROWS = 128  # DOL_SLAB_ROWS: rows per row group of the chunk-major packing
 
 
 def csr_slab_pack(rowptr: torch.Tensor, col: torch.Tensor, val: torch.Tensor, x_rows: int,
-                  ent: Optional[torch.Tensor] = None, hdr: Optional[torch.Tensor] = None):
+                  ent: Optional[torch.Tensor] = None, hdr: Optional[torch.Tensor] = None, balance: bool = False):
     """(ent, hdr) of a device CSR for mix_csr_slab (dol_csr_slab_pack): the
-    entries re-packed chunk-major per group of SLAB_ROWS rows as (LDS byte
-    offset, weight bits) pairs, every (row, chunk) segment padded to an even
-    length; hdr[g][k][i] = first entry of row g*ROWS+i in chunk k, bit 0 = the
-    segment ends in a pad.  col/val may be longer than nnz (a capacity); ent
-    is sized from it."""
+    rows of each group of SLAB_ROWS dealt to slots (balanced per-chunk wave
+    loads), the entries re-packed chunk-major as (weight bits, LDS byte offset)
+    pairs, every (slot, chunk) segment padded to an even length; hdr[g][k][s] =
+    first entry of slot s in chunk k, bit 0 = the segment ends in a pad, then
+    perm[g][s] = row and inv[row] = slot (include/dol_hip.h).  col/val may be
+    longer than nnz (a capacity); ent is sized from it.  balance: deal the
+    rows to the kernel's waves by greedy packing of their per-chunk loads
+    (same bits; worth it when one W is mixed many times)."""
     n = rowptr.numel() - 1
     _check_csr(rowptr, col, val, rowptr.device)
     L = _native.lib()
@@ -144,8 +147,8 @@ def csr_slab_pack(rowptr: torch.Tensor, col: torch.Tensor, val: torch.Tensor, x_
     if hdr is None or hdr.numel() < need_h:
         hdr = torch.empty(max(need_h, 4), dtype=torch.int32, device=rowptr.device)
     _native.call("dol_csr_slab_pack", rowptr.data_ptr(), col.data_ptr() if col.numel() else None,
-                 val.data_ptr() if val.numel() else None, n, int(x_rows), ent.data_ptr(), hdr.data_ptr(),
-                 _stream(rowptr))
+                 val.data_ptr() if val.numel() else None, n, int(x_rows), int(bool(balance)), ent.data_ptr(),
+                 hdr.data_ptr(), _stream(rowptr))
     return ent, hdr
 
 

@@ -267,6 +267,11 @@ def global_mean(local_rows: torch.Tensor, local_order: Sequence[int], m_total: i
     device = local_rows.device
     if out is None:
         out = torch.empty(P, dtype=torch.float32, device=device)
+    sharded = dist.is_initialized() and dist.get_world_size(group) > 1
+    if not sharded and len(local_order):  # one pass: the sum, then / m in the same kernel
+        idx = (local_order if isinstance(local_order, torch.Tensor) and local_order.device == device
+               else torch.as_tensor(list(local_order), dtype=torch.int32, device=device))
+        return ordered_sum(local_rows, idx, out=out, scale=float(m_total), P=P)
     if len(local_order):
         if isinstance(local_order, torch.Tensor) and local_order.device == device:
             idx = local_order

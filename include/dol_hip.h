@@ -80,16 +80,21 @@ int dol_mix_csr_pm_f32(const float* XT, int64_t ldx, int32_t x_rows, float* YT, 
  * rounding, bit-identical results.  X's columns stream through LDS in chunks
  * of DOL_SLAB_CHUNK agents; each row's neighbour sum is gathered from LDS in
  * ascending column order.  The CSR comes re-packed chunk-major by
- * dol_csr_slab_pack (rows in groups of DOL_SLAB_ROWS; for group g and chunk k
- * the entries of the group's rows with columns in the chunk are contiguous):
- *   ent  int32 [dol_csr_slab_ent_len(nnz, n_rows, x_rows)]: (LDS byte offset,
- *        weight bits) entries stored in pairs as (offset 0, offset 1, weight 0,
- *        weight 1); every (row, chunk) segment padded to an even number of
- *        entries with a (65536, 0) entry, which the kernel reads from a zero
+ * dol_csr_slab_pack (rows in groups of DOL_SLAB_ROWS, each row dealt to a
+ * SLOT of its group so the kernel's 16 waves get even per-chunk loads; for
+ * group g and chunk k the entries of the group's slots with columns in the
+ * chunk are contiguous, in slot order):
+ *   ent  int32 [dol_csr_slab_ent_len(nnz, n_rows, x_rows)]: (weight bits, LDS
+ *        byte offset) entries stored in pairs as (weight 0, offset 0, weight 1,
+ *        offset 1); every (slot, chunk) segment padded to an even number of
+ *        entries with a (0, 65536) entry, which the kernel reads from a zero
  *        piece in LDS (its +0 product leaves every sum's bits unchanged)
- *   hdr  int32 [dol_csr_slab_hdr_len(n_rows, x_rows)]: hdr[g][k][i] = ent
- *        index of row g*DOL_SLAB_ROWS+i's first entry in chunk k (i <= ROWS;
- *        even), bit 0 set when that segment ends in a pad entry
+ *   hdr  int32 [dol_csr_slab_hdr_len(n_rows, x_rows)]: hdr[g][k][s] = ent
+ *        index of slot s's first entry in chunk k (s <= ROWS; even), bit 0 set
+ *        when that segment ends in a pad entry; then perm[g][s] = the row in
+ *        slot s of group g (-1: none) and inv[row] = its slot
+ * A row's entries keep their ascending column order whatever its slot, so the
+ * sums (and bits) do not depend on the dealing.
  * Limits: ldx, ldy multiples of 4, ldx >= round_up(P, 4) (X rows readable in
  * whole 16-B pieces), X, Y and ent 16-B aligned, X and Y not aliased.
  */
@@ -101,9 +106,13 @@ int64_t dol_csr_slab_ent_len(int64_t nnz_capacity, int32_t n_rows, int32_t x_row
 int dol_mix_csr_slab_f32(const float* X, int64_t ldx, int32_t x_rows, float* Y, int64_t ldy, int32_t n_rows,
                          int64_t P, const int32_t* ent, const int32_t* hdr, hipStream_t s);
 /* ent and hdr (above) of a device CSR (rowptr / col / val as dol_mix_csr_f32,
- * 0 <= col < x_rows); ent sized for the CSR's nnz (or a capacity >= nnz). */
+ * 0 <= col < x_rows); ent sized for the CSR's nnz (or a capacity >= nnz).
+ * balance = 0: slots in row order; 1: rows dealt to the 16 waves by greedy
+ * vector packing of their per-chunk entry counts (x_rows <= 32768; measured
+ * 0.5-1 % off the mix at 1024 x 101,770 ER p = 0.1 for 0.13 ms of packing, so
+ * worth it only when one W is mixed many times). */
 int dol_csr_slab_pack(const int32_t* rowptr, const int32_t* col, const float* val, int32_t n_rows,
-                      int32_t x_rows, int32_t* ent, int32_t* hdr, hipStream_t s);
+                      int32_t x_rows, int32_t balance, int32_t* ent, int32_t* hdr, hipStream_t s);
 /*
  * Neighbors (DIST/simulators.py:91-97) of every row of a dense device W, on
  * the device: rowptr[n_rows + 1] and col / val (capacity cap >= n_rows *

@@ -100,25 +100,66 @@ def test_slab_rectangular_and_low_degree_rows(gpu):
     assert bits_equal(Yd.cpu().numpy(), oracle.mix_csr(X, csr.rowptr, csr.col, csr.val))
 
 
-def slab_pack_host(csr, x_rows):
-    """Host restatement of dol_csr_slab_pack: rows in groups of SLAB_ROWS; for
-    group g, chunk k the rows' chunk-k entries contiguous in (row, column)
-    order, each row's segment padded to an even length with a pad entry (offset
-    SLAB_ZERO_OFFSET = the stage's zero piece, weight 0); entry = (LDS byte
-    offset (col % 64) * 1024, weight bits); entries stored in PAIRS as (offset
-    0, offset 1, weight 0, weight 1); header word = segment start | (1 if
-    padded).  Returns (hdr, entries as an [n, 2] (offset, weight) array)."""
+def slab_balance_host(counts):
+    """Host restatement of slab_balance_kernel for one row group: counts[i, k]
+    = padded entries of row i in chunk k.  Rows by total (descending, ties by
+    index), each to the wave (< RW rows) minimising sum_k c_k (2 L_wk + c_k)
+    (ties: lowest wave); slot = wave * RW + the wave's fill.  Returns slot[i]."""
+    R, WV = counts.shape[0], 16
+    RW = R // WV
+    tot = counts.sum(1)
+    order = sorted(range(R), key=lambda i: (-tot[i], i))
+    L = np.zeros((WV, counts.shape[1]), np.int64)
+    fill = np.zeros(WV, np.int64)
+    slot = np.zeros(R, np.int64)
+    for i in order:
+        c = counts[i].astype(np.int64)
+        cost = [(int((c * (2 * L[w] + c)).sum()), w) for w in range(WV) if fill[w] < RW]
+        w = min(cost)[1]
+        slot[i] = w * RW + fill[w]
+        fill[w] += 1
+        L[w] += c
+    return slot
+
+
+def slab_pack_host(csr, x_rows, balance=False):
+    """Host restatement of dol_csr_slab_pack: rows in groups of SLAB_ROWS, dealt
+    to slots by slab_balance_host (balance) or in row order; for group g, chunk k the slots' chunk-k
+    entries contiguous in (slot, column) order, each segment padded to an even
+    length with a pad entry (offset SLAB_ZERO_OFFSET = the stage's zero piece,
+    weight 0); entry = (LDS byte offset (col % 64) * 1024, weight bits); entries
+    stored in PAIRS as (weight 0, offset 0, weight 1, offset 1); header word =
+    segment start | (1 if padded); then perm[g][slot] = row (-1: none) and
+    inv[row] = slot.  Returns (hdr blocks, entries as an [n, 2] (offset, weight)
+    array, perm, inv)."""
     R, C = ops.SLAB_ROWS, ops.SLAB_CHUNK
     nk = -(-x_rows // C)
     n_rg = -(-csr.n_rows // R)
     hdr = np.zeros((n_rg, nk, R + 1), np.int64)
+    perm = np.full((n_rg, R), -1, np.int64)
+    inv = np.zeros(n_rg * R, np.int64)
     ent = []
     for g in range(n_rg):
+        sel_rows = {}
+        counts = np.zeros((R, nk), np.int64)
+        for i in range(R):
+            r = g * R + i
+            if r < csr.n_rows:
+                cols = csr.col[csr.rowptr[r]:csr.rowptr[r + 1]]
+                for k in range(nk):
+                    n = int(((cols >= k * C) & (cols < (k + 1) * C)).sum())
+                    counts[i, k] = n + (n & 1)
+        slot = slab_balance_host(counts) if balance else np.arange(R)
+        for i in range(R):
+            r = g * R + i
+            if r < csr.n_rows:
+                perm[g, slot[i]] = r
+                inv[r] = slot[i]
         for k in range(nk):
-            for i in range(R + 1):
-                hdr[g, k, i] = len(ent)
-                r = g * R + i
-                if i == R or r >= csr.n_rows:
+            for sl in range(R + 1):
+                hdr[g, k, sl] = len(ent)
+                r = perm[g, sl] if sl < R else -1
+                if r < 0:
                     continue
                 cols = csr.col[csr.rowptr[r]:csr.rowptr[r + 1]]
                 vals = csr.val[csr.rowptr[r]:csr.rowptr[r + 1]]
@@ -127,23 +168,66 @@ def slab_pack_host(csr, x_rows):
                     ent.append(((int(c) % C) * 1024, int(np.float32(v).view(np.int32))))
                 if sel.sum() % 2:
                     ent.append((SLAB_ZERO_OFFSET, 0))
-                    hdr[g, k, i] |= 1
-    return hdr, np.array(ent, np.int64).reshape(-1, 2)
+                    hdr[g, k, sl] |= 1
+    return hdr, np.array(ent, np.int64).reshape(-1, 2), perm, inv[:csr.n_rows]
 
 
 SLAB_ZERO_OFFSET = 64 * 1024  # csr_slab.hip kZeroRel: the zero piece after each 64-KiB X stage
 
 
-@pytest.mark.parametrize("n,p", [(200, 0.2), (300, 0.05)])
-def test_slab_pack_matches_host(n, p, gpu):
+@pytest.mark.parametrize("balance", [False, True])
+@pytest.mark.parametrize("n,p", [(200, 0.2), (300, 0.05), (1024, 0.1)])
+def test_slab_pack_matches_host(n, p, balance, gpu):
     csr = er_csr(n, p, seed=3, empty_rows=(7,))
     plan = G.MixingPlan(csr, gpu, slab=True)
-    hdr, ent = slab_pack_host(csr, n)
-    got_h = plan.hdr[: hdr.size].cpu().numpy().reshape(hdr.shape)
-    assert np.array_equal(got_h, hdr)
-    pairs = plan.ent[: 2 * len(ent)].cpu().numpy().reshape(-1, 4)  # (off0, off1, w0, w1)
-    got_e = np.stack([pairs[:, [0, 1]].reshape(-1), pairs[:, [2, 3]].reshape(-1)], axis=1)
+    rp, col, val = (torch.as_tensor(a, device=gpu) for a in (csr.rowptr, csr.col, csr.val))
+    ent_d, hdr_d = ops.csr_slab_pack(rp, col, val, n, balance=balance)
+    hdr, ent, perm, inv = slab_pack_host(csr, n, balance)
+    H = hdr_d.cpu().numpy()
+    nb = hdr.size
+    assert np.array_equal(H[:nb].reshape(hdr.shape), hdr)
+    assert np.array_equal(H[nb:nb + perm.size].reshape(perm.shape), perm)
+    assert np.array_equal(H[nb + perm.size:nb + perm.size + n], inv)
+    pairs = ent_d[: 2 * len(ent)].cpu().numpy().reshape(-1, 4)  # (w0, off0, w1, off1)
+    got_e = np.stack([pairs[:, [1, 3]].reshape(-1), pairs[:, [0, 2]].reshape(-1)], axis=1)
     assert np.array_equal(got_e, ent)
+
+
+@pytest.mark.parametrize("n,P,p", [(1024, 2560, 0.1), (300, 1001, 0.3)])
+def test_slab_balanced_pack_mixes_bit_exactly(n, P, p, gpu):
+    """Rows dealt to waves by the greedy packing: the same sums in the same
+    order, so the same bits as the row-order packing and the oracle."""
+    csr = er_csr(n, p, seed=n + 7, empty_rows=(2,))
+    rp, col, val = (torch.as_tensor(a, device=gpu) for a in (csr.rowptr, csr.col, csr.val))
+    ent, hdr = ops.csr_slab_pack(rp, col, val, n, balance=True)
+    X = special_x(n, P, seed=P + 1)
+    ld = -(-P // 4) * 4
+    Xd, Yd = bank_like(X, gpu, ld), bank_like(np.zeros_like(X), gpu, ld)
+    ops.mix_csr_slab(Xd, Yd, ent, hdr, n, x_rows=n, P=P)
+    torch.cuda.synchronize()
+    assert bits_equal(Yd[:, :P].cpu().numpy(), oracle.mix_csr(X, csr.rowptr, csr.col, csr.val))
+
+
+def test_slab_balancing_evens_the_chunk_loads():
+    """The balancing's point (host restatement, the kernel is pinned to it
+    above): at ER p = 0.1, 1024 agents, the sum over chunks of the busiest
+    wave's entries drops well below row-order dealing."""
+    rng = np.random.default_rng(1)
+    n, R, C, WV = 1024, ops.SLAB_ROWS, ops.SLAB_CHUNK, 16
+    A = rng.random((n, n)) < 0.1
+    np.fill_diagonal(A, False)
+    cnt = A.reshape(n, n // C, C).sum(2)
+    cnt = cnt + (cnt & 1)
+    natural = balanced = 0
+    for g in range(n // R):
+        c = cnt[g * R:(g + 1) * R]
+        natural += c.reshape(WV, R // WV, -1).sum(1).max(0).sum()
+        slot = slab_balance_host(c)
+        L = np.zeros((WV, c.shape[1]), np.int64)
+        for i in range(R):
+            L[slot[i] // (R // WV)] += c[i]
+        balanced += L.max(0).sum()
+    assert balanced < 0.93 * natural
 
 
 @pytest.mark.parametrize("n,p", [(1024, 0.1), (333, 0.5)])
