@@ -384,6 +384,114 @@ __global__ __launch_bounds__(kThreads) void ring_steps_kernel(
 }
 
 // ----------------------------------------------------------------------------
+// Streaming temporal blocking (r03): the same STEPS synchronous rounds and the
+// same bits as ring_steps_kernel, with each thread walking ONE f4 column down
+// a tile of T rows (+ STEPS halo rows on each side) instead of holding the
+// whole tile in registers: when level-0 row i arrives, level t is produced at
+// index i - t from level t-1's values at i - t + 1 (this step) and i - t - 1
+// (two steps ago), so each level keeps its last two values (the step parity
+// picks the register set: no copies) and the loads run PF rows ahead.  HBM
+// sees one continuous read stream per column (halo re-reads 2 STEPS / T of
+// the tile, from L2: vertically adjacent tiles run back to back on one XCD)
+// instead of ring_steps_kernel's load-all / compute / store bursts with 2
+// STEPS / R = 45 % halo at R = 22.  The stencil has no diagonal term (circle
+// W: W_ii = 0), so only the two neighbours enter, as in axpy0.
+// ----------------------------------------------------------------------------
+template <int S, int PF, bool INTERIOR, bool NT>
+__device__ __forceinline__ void ring_stream_body(const f4* __restrict__ xc, int64_t ldv, float* __restrict__ Y,
+                                                 int64_t ldy, int64_t c, int n_rows, int r0, int nT,
+                                                 const float* __restrict__ wprev, const float* __restrict__ wnext) {
+  const int nsteps = nT + 2 * S;
+  auto wrap = [&](int g) {  // |g| within one ring length of [0, n_rows)
+    if constexpr (!INTERIOR) g = g < 0 ? g + n_rows : (g >= n_rows ? g - n_rows : g);
+    return g;
+  };
+  // the prefetch walks the input rows with a running pointer (one 64-bit add per
+  // step, a wrap test on edge tiles); past the tile's last input row it stays on
+  // that row (always valid, never used)
+  int gl = wrap(r0 - S);
+  const f4* lp = xc + int64_t(gl) * ldv;
+  int left = nsteps;  // input rows not yet issued
+  auto next = [&]() {
+    const f4 v = NT ? __builtin_nontemporal_load(lp) : *lp;
+    if (--left > 0) {
+      ++gl;
+      lp += ldv;
+      if constexpr (!INTERIOR) {
+        if (gl == n_rows) {
+          gl = 0;
+          lp = xc;
+        }
+      }
+    }
+    return v;
+  };
+  f4 pf[PF];
+#pragma unroll
+  for (int u = 0; u < PF; ++u) pf[u] = next();
+  f4 hA[S], hB[S];  // level t's value from two steps back, even / odd steps
+#pragma unroll
+  for (int t = 0; t < S; ++t) hA[t] = hB[t] = f4{0.f, 0.f, 0.f, 0.f};
+  f4* yp = reinterpret_cast<f4*>(Y + int64_t(r0) * ldy) + c;  // the next output row
+  const int64_t ldyv = ldy / 4;
+  struct Wn { float v[PF + S]; };  // the weights of rows r0 - 2S + i0 .. (one scalar load per array and PF steps)
+  for (int i0 = 0; i0 < nsteps; i0 += PF) {
+    Wn wp, wn;
+    if constexpr (INTERIOR) {
+      wp = *reinterpret_cast<const Wn*>(wprev + (r0 - 2 * S + i0));
+      wn = *reinterpret_cast<const Wn*>(wnext + (r0 - 2 * S + i0));
+    } else {
+#pragma unroll
+      for (int j = 0; j < PF + S; ++j) {
+        const int g = wrap(r0 - 2 * S + min(i0 + j, nsteps + S - 1));
+        wp.v[j] = wprev[g];
+        wn.v[j] = wnext[g];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      const int i = i0 + u;
+      f4 nv = pf[u];  // level 0 at index i
+      pf[u] = next();
+#pragma unroll
+      for (int t = 1; t <= S; ++t) {
+        f4& hv = (u & 1) ? hB[t - 1] : hA[t - 1];
+        const f4 old = hv;  // level t-1 at index i - t - 1
+        hv = nv;            // level t-1 at index i - t + 1, for two steps on
+        // row of index i - t = r0 - 2S + i0 + (u + S - t)
+        nv = axpy0(wp.v[u + S - t], old, wn.v[u + S - t], nv);
+      }
+      if (i >= 2 * S && i < nsteps) {  // level S at index i - S = row r0 + i - 2S
+        __builtin_nontemporal_store(nv, yp);
+        yp += ldyv;
+      }
+    }
+  }
+}
+
+template <int S, int T, int PF, bool NT>
+__global__ __launch_bounds__(kThreads) void ring_stream_kernel(
+    const float* __restrict__ X, int64_t ldx, float* __restrict__ Y, int64_t ldy, int n_rows,
+    int64_t ncols_v, uint32_t n_col_tiles, const float* __restrict__ wprev,
+    const float* __restrict__ wnext, uint32_t n_row_tiles) {
+  static_assert(PF % 2 == 0, "the step parity selects the history registers");
+  const uint32_t b = blockIdx.x;
+  const uint32_t x = b & 7u, l = b >> 3;
+  const uint32_t ct = (l / n_row_tiles) * 8 + x;
+  const int r0 = static_cast<int>(l % n_row_tiles) * T;
+  if (ct >= n_col_tiles) return;
+  const int64_t c = int64_t(ct) * kThreads + threadIdx.x;
+  if (c >= ncols_v) return;
+  const int nT = min(T, n_rows - r0);
+  const f4* xc = reinterpret_cast<const f4*>(X) + c;
+  const int64_t ldv = ldx / 4;
+  if (r0 - S >= 0 && r0 + nT + S + PF <= n_rows)
+    ring_stream_body<S, PF, true, NT>(xc, ldv, Y, ldy, c, n_rows, r0, nT, wprev, wnext);
+  else
+    ring_stream_body<S, PF, false, NT>(xc, ldv, Y, ldy, c, n_rows, r0, nT, wprev, wnext);
+}
+
+// ----------------------------------------------------------------------------
 // Generic CSR mix.  Blocks are ordered row-group fastest so that all rows of
 // one column tile are in flight together: a neighbour row segment fetched
 // from HBM by one workgroup is re-read from L2 / Infinity Cache by the others.
@@ -1349,8 +1457,45 @@ int dol_mix_ring_steps_f32(const float* X, int64_t ldx, float* Y, int64_t ldy, i
   if (steps == 0) return fail(DOL_EINVAL, "dol_mix_ring_steps_f32: steps must be >= 1");
   const bool vec = row_vec_ok(X, ldx) && row_vec_ok(Y, ldy) && P % 4 == 0;
   if (!vec || steps > 8) return fail(DOL_EINVAL, "dol_mix_ring_steps_f32: needs 16-B aligned rows, P %% 4 == 0 and steps <= 8 (compose launches otherwise)");
+  // ring_stream_kernel (1024-row tiles, 8 rows in flight, nontemporal loads)
+  // unless DOL_RING_STREAM=0 (the register-tile ring_steps_kernel).  eps = 5 at
+  // 8192 x 2^20, alternating on one box (profiles/r03_eps_stream.txt): box A
+  // stream 12.38 / 12.39 vs tiles 12.61 / 12.62 ms; box B stream-NT 11.60 /
+  // 12.00 / 11.76 vs tiles 11.90 / 11.92 / 11.80 (ring round 11.7-12.0 there):
+  // both at the ring round's rate, the clock 1 % below it (2424 / 2408 vs 2439
+  // MHz, GRBM_GUI_ACTIVE per XCD over the kernel's time).
+  static const int stream = [] { const char* e = getenv("DOL_RING_STREAM"); return e ? atoi(e) : 1; }();
+  static const int stream_t = [] { const char* e = getenv("DOL_RING_STREAM_T"); return e ? atoi(e) : 1024; }();
+  static const int stream_pf = [] { const char* e = getenv("DOL_RING_STREAM_PF"); return e ? atoi(e) : 8; }();
+  static const int stream_nt = [] { const char* e = getenv("DOL_RING_STREAM_NT"); return e ? atoi(e) : 1; }();
+  auto go_stream_pf = [&](auto steps_c, auto t_c, auto pf_c) {
+    constexpr int S = decltype(steps_c)::value, T = decltype(t_c)::value, PF = decltype(pf_c)::value;
+    const int64_t nv = P / 4;
+    const uint32_t nct = static_cast<uint32_t>(cdiv(nv, kThreads));
+    const int64_t nrt = cdiv(n_rows, T);
+    const int64_t grid = cdiv(nct, 8) * 8 * nrt;
+    if (grid > kMaxBlocks) return fail(DOL_EINVAL, "dol_mix_ring_steps_f32: too large");
+    if (stream_nt)
+      hipLaunchKernelGGL((ring_stream_kernel<S, T, PF, true>), dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, s, X,
+                         ldx, Y, ldy, n_rows, nv, nct, w_prev, w_next, static_cast<uint32_t>(nrt));
+    else
+      hipLaunchKernelGGL((ring_stream_kernel<S, T, PF, false>), dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, s, X,
+                         ldx, Y, ldy, n_rows, nv, nct, w_prev, w_next, static_cast<uint32_t>(nrt));
+    return check_launch("dol_mix_ring_steps_f32");
+  };
+  auto go_stream = [&](auto steps_c, auto t_c) {
+    constexpr int S = decltype(steps_c)::value, T = decltype(t_c)::value;
+    if (stream_pf == 16) return go_stream_pf(steps_c, t_c, std::integral_constant<int, 16>{});
+    return go_stream_pf(steps_c, t_c, std::integral_constant<int, 8>{});
+  };
+
   auto go_v = [&](auto steps_c, auto r_c, auto v_c) {
     constexpr int S = decltype(steps_c)::value, R = decltype(r_c)::value;
+    if (stream && n_rows >= 2 * S + 16 + 1) {  // the stream kernel wraps at most once (PF <= 16)
+      using std::integral_constant;
+      if (stream_t == 2048) return go_stream(steps_c, integral_constant<int, 2048>{});
+      return go_stream(steps_c, integral_constant<int, 1024>{});  // 256 / 512 / 4096-row tiles measured slower
+    }
     using V = typename decltype(v_c)::type;
     const int64_t nv = P / Vec<V>::W;
     const uint32_t nct = static_cast<uint32_t>(cdiv(nv, kThreads));

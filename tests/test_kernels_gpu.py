@@ -588,8 +588,12 @@ def test_prox_grad_term_vs_oracle(admm, extra, gpu):
 
 
 @pytest.mark.parametrize("steps", [1, 2, 3, 4, 5, 6, 7, 8])
-@pytest.mark.parametrize("n,P", [(3, 8), (17, 4100), (64, 1024 * 5), (200, 1024), (1001, 2048)])
+@pytest.mark.parametrize("n,P", [(3, 8), (17, 4100), (64, 1024 * 5), (200, 1024), (1001, 2048), (1600, 4100),
+                                 (2048, 1024)])
 def test_ring_steps_bit_identical_to_single_rounds(steps, n, P, gpu):
+    """ring_stream_kernel (n >= 2 steps + 9; 512-row tiles: 1600 / 2048 rows have
+    interior tiles, wrap-around edge tiles and a short last tile) and the
+    register-tile kernel (smaller rings)."""
     rng = np.random.default_rng(steps * 100 + n)
     X = rng.standard_normal((n, P)).astype(np.float32)
     wp, wn = rng.random(n).astype(np.float32), rng.random(n).astype(np.float32)
