@@ -412,7 +412,7 @@ __device__ __forceinline__ void bstore_nt(rsrc_t r, uint32_t voff, uint32_t soff
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, static_cast<int>(voff), static_cast<int>(soff), 2);
 }
 
-template <int KS, int UPD, bool TH, bool AL>
+template <int KS, int UPD, bool TH, bool AL, int CH = 1>
 __global__ __launch_bounds__(kThreads) void mlp_dw1_kernel(MlpArgs a, const float* __restrict__ ws) {
   const int B = a.B, d = a.d, h = a.h, c = a.c;
   const int ndt = (d + 31) / 32;
@@ -457,8 +457,18 @@ __global__ __launch_bounds__(kThreads) void mlp_dw1_kernel(MlpArgs a, const floa
     f32x16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    if constexpr (CH == 2) {  // two independent k-chains (even / odd k-steps), summed at the end
+      f32x16 acc1 = acc;
 #pragma unroll
-    for (int s = 0; s < KS; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], xv[s], acc, 0, 0, 0);
+      for (int s = 0; s < KS; s += 2) {
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], xv[s], acc, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s + 1], xv[s + 1], acc1, 0, 0, 0);
+      }
+      acc += acc1;
+    } else {
+#pragma unroll
+      for (int s = 0; s < KS; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[s], xv[s], acc, 0, 0, 0);
+    }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       float gg = acc[r];
@@ -532,6 +542,11 @@ extern "C" int dol_mlp_step_f32(float* w, int64_t ldw, float* grad, int64_t ldg,
   const int64_t n_blk2 = int64_t((d + 31) / 32) * n_agents;
   if (n_blk2 > (int64_t(1) << 31) - 1) return fail(DOL_EINVAL, "dol_mlp_step_f32: too many W1 tiles for one launch");
   const dim3 grid2(static_cast<unsigned>(n_blk2));
+  // dW1's k-chain as two interleaved accumulators summed at the end (VERDICT r02
+  // item 4): local step 0.5036-0.5046 vs 0.5074-0.5079 ms with one chain, three
+  // alternating pairs on one box (profiles/r03_mlp_dw1_chains.txt) -- the step
+  // is not chain-latency bound; DOL_MLP_DW1_CHAINS=1 restores one chain
+  static const int dw1_chains = [] { const char* e = getenv("DOL_MLP_DW1_CHAINS"); return e ? atoi(e) : 2; }();
   auto go = [&](auto ks, auto upd_c, auto th, auto al) {
     constexpr int KS = decltype(ks)::value, U = decltype(upd_c)::value;
     constexpr bool TH = decltype(th)::value, AL = decltype(al)::value;
@@ -555,7 +570,10 @@ extern "C" int dol_mlp_step_f32(float* w, int64_t ldw, float* grad, int64_t ldg,
       if (nt1) fwd(mlp_fwd_kernel<1, U, TH, AL>, lds);
       else fwd(mlp_fwd_kernel<4, U, TH, AL>, lds);
     }
-    hipLaunchKernelGGL((mlp_dw1_kernel<KS, U, TH, AL>), grid2, block, 0, s, a, ws);
+    if (dw1_chains == 2)
+      hipLaunchKernelGGL((mlp_dw1_kernel<KS, U, TH, AL, 2>), grid2, block, 0, s, a, ws);
+    else
+      hipLaunchKernelGGL((mlp_dw1_kernel<KS, U, TH, AL>), grid2, block, 0, s, a, ws);
   };
   auto by_upd = [&](auto ks, auto th, auto al) {
     using std::integral_constant;
