@@ -469,11 +469,11 @@ __device__ __forceinline__ void ring_stream_body(const f4* __restrict__ xc, int6
   }
 }
 
-template <int S, int T, int PF, bool NT>
+template <int S, int PF, bool NT>
 __global__ __launch_bounds__(kThreads) void ring_stream_kernel(
     const float* __restrict__ X, int64_t ldx, float* __restrict__ Y, int64_t ldy, int n_rows,
     int64_t ncols_v, uint32_t n_col_tiles, const float* __restrict__ wprev,
-    const float* __restrict__ wnext, uint32_t n_row_tiles) {
+    const float* __restrict__ wnext, uint32_t n_row_tiles, int T) {
   static_assert(PF % 2 == 0, "the step parity selects the history registers");
   const uint32_t b = blockIdx.x;
   const uint32_t x = b & 7u, l = b >> 3;
@@ -485,7 +485,7 @@ __global__ __launch_bounds__(kThreads) void ring_stream_kernel(
   const int nT = min(T, n_rows - r0);
   const f4* xc = reinterpret_cast<const f4*>(X) + c;
   const int64_t ldv = ldx / 4;
-  if (r0 - S >= 0 && r0 + nT + S + PF <= n_rows)
+  if (r0 - 2 * S >= 0 && r0 + nT + S + PF <= n_rows)  // every row and weight index in range
     ring_stream_body<S, PF, true, NT>(xc, ldv, Y, ldy, c, n_rows, r0, nT, wprev, wnext);
   else
     ring_stream_body<S, PF, false, NT>(xc, ldv, Y, ldy, c, n_rows, r0, nT, wprev, wnext);
@@ -1468,33 +1468,31 @@ int dol_mix_ring_steps_f32(const float* X, int64_t ldx, float* Y, int64_t ldy, i
   static const int stream_t = [] { const char* e = getenv("DOL_RING_STREAM_T"); return e ? atoi(e) : 1024; }();
   static const int stream_pf = [] { const char* e = getenv("DOL_RING_STREAM_PF"); return e ? atoi(e) : 8; }();
   static const int stream_nt = [] { const char* e = getenv("DOL_RING_STREAM_NT"); return e ? atoi(e) : 1; }();
-  auto go_stream_pf = [&](auto steps_c, auto t_c, auto pf_c) {
-    constexpr int S = decltype(steps_c)::value, T = decltype(t_c)::value, PF = decltype(pf_c)::value;
+  auto go_stream_pf = [&](auto steps_c, int T, auto pf_c) {
+    constexpr int S = decltype(steps_c)::value, PF = decltype(pf_c)::value;
     const int64_t nv = P / 4;
     const uint32_t nct = static_cast<uint32_t>(cdiv(nv, kThreads));
     const int64_t nrt = cdiv(n_rows, T);
     const int64_t grid = cdiv(nct, 8) * 8 * nrt;
     if (grid > kMaxBlocks) return fail(DOL_EINVAL, "dol_mix_ring_steps_f32: too large");
     if (stream_nt)
-      hipLaunchKernelGGL((ring_stream_kernel<S, T, PF, true>), dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, s, X,
-                         ldx, Y, ldy, n_rows, nv, nct, w_prev, w_next, static_cast<uint32_t>(nrt));
+      hipLaunchKernelGGL((ring_stream_kernel<S, PF, true>), dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, s, X,
+                         ldx, Y, ldy, n_rows, nv, nct, w_prev, w_next, static_cast<uint32_t>(nrt), T);
     else
-      hipLaunchKernelGGL((ring_stream_kernel<S, T, PF, false>), dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, s, X,
-                         ldx, Y, ldy, n_rows, nv, nct, w_prev, w_next, static_cast<uint32_t>(nrt));
+      hipLaunchKernelGGL((ring_stream_kernel<S, PF, false>), dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, s, X,
+                         ldx, Y, ldy, n_rows, nv, nct, w_prev, w_next, static_cast<uint32_t>(nrt), T);
     return check_launch("dol_mix_ring_steps_f32");
   };
-  auto go_stream = [&](auto steps_c, auto t_c) {
-    constexpr int S = decltype(steps_c)::value, T = decltype(t_c)::value;
-    if (stream_pf == 16) return go_stream_pf(steps_c, t_c, std::integral_constant<int, 16>{});
-    return go_stream_pf(steps_c, t_c, std::integral_constant<int, 8>{});
+  auto go_stream = [&](auto steps_c, int T) {
+    if (stream_pf == 16) return go_stream_pf(steps_c, T, std::integral_constant<int, 16>{});
+    if (stream_pf == 4) return go_stream_pf(steps_c, T, std::integral_constant<int, 4>{});
+    return go_stream_pf(steps_c, T, std::integral_constant<int, 8>{});
   };
 
   auto go_v = [&](auto steps_c, auto r_c, auto v_c) {
     constexpr int S = decltype(steps_c)::value, R = decltype(r_c)::value;
     if (stream && n_rows >= 2 * S + 16 + 1) {  // the stream kernel wraps at most once (PF <= 16)
-      using std::integral_constant;
-      if (stream_t == 2048) return go_stream(steps_c, integral_constant<int, 2048>{});
-      return go_stream(steps_c, integral_constant<int, 1024>{});  // 256 / 512 / 4096-row tiles measured slower
+      return go_stream(steps_c, stream_t >= 64 ? stream_t : 1024);
     }
     using V = typename decltype(v_c)::type;
     const int64_t nv = P / Vec<V>::W;

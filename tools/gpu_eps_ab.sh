@@ -7,7 +7,7 @@ mkdir -p "$OUT"
 for rep in ${REPS:-1 2}; do
   for v in ${VARIANTS:-DOL_RING_STREAM=0 DOL_RING_STREAM_T=1024 DOL_RING_STREAM_T=2048 DOL_RING_STREAM_T=4096 DOL_RING_STREAM_PF=16}; do
     echo "# $v" >> "$OUT/eps.jsonl"
-    env $v timeout -k 10 120 python -u tools/eps_pass_time.py --eps ${EPS:-5} >> "$OUT/eps.jsonl" 2>> "$OUT/eps.err"
+    env $(echo $v | tr , " ") timeout -k 10 120 python -u tools/eps_pass_time.py --eps ${EPS:-5} >> "$OUT/eps.jsonl" 2>> "$OUT/eps.err"
     rc=$?; [ $rc -eq 0 ] || { echo "rc=$rc"; tail -3 "$OUT/eps.err"; exit $rc; }
   done
 done
