@@ -375,7 +375,7 @@ def er_exact_mix_round(device, N: int = 1024, P: int = 101770, reps: int = 10):
     return {"agents": N, "params": P, "nnz": nnz, "ms_per_round": ms_round, "rounds_per_s": 1e3 / ms_round,
             "mix_ms": ms_mix, "lds_GBps": nnz * P * 4 / (ms_mix / 1e3) / 1e9,
             "kernel": "csr_slab_kernel (LDS-gather CSR) + dense_to_csr + slab_pack",
-            "what": "the same time-varying ER p=0.1 W as dense_er_mix, mixed bit-exactly (reference consensus order); "
+            "what": "a time-varying ER p=0.1 W (drawn each round by the device hash kernel; dense_er_mix draws its W with the torch generator, same distribution), mixed bit-exactly (reference consensus order); "
                     "W draw + device Neighbors + packing included in ms_per_round"}
 
 

@@ -176,7 +176,12 @@ __host__ __device__ inline int64_t fwd_union_floats(int B, int h, int c, int ns 
 // deep; a row-contiguous load touches 8 lines per instruction where reading
 // the MFMA fragments straight from HBM touched 64 (2.3 TB/s effective).
 // NT = accumulator tiles per wave: 1 when h * ceil(B/32) <= 128, else 4.
-template <int NT, int UPD, bool TH, bool AL, int NS = kStages>
+// PH (r03): 0 = the whole per-agent part in one kernel; 1 = F1 only, H (after
+// bias + relu) to ws[agent][b][h] (LDS = the F1 staging alone); 2 = the rest
+// (F2, CE, B2, dZ1 -> ws) from that H.  1 + 2 run the same operations in the
+// same order as 0 (bit-identical); the split lets F1 stream W1 without the
+// HBM-idle tail and with deeper staging.
+template <int NT, int UPD, bool TH, bool AL, int NS = kStages, int PH = 0>
 __global__ __launch_bounds__(kThreads) void mlp_fwd_kernel(MlpArgs a, float* __restrict__ ws) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int B = a.B, d = a.d, h = a.h, c = a.c;
@@ -211,13 +216,20 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd_kernel(MlpArgs a, float* __r
   auto idx_b2 = [&](int) { return ob2 + (t < c ? t : 0); };
   ParamBatch<8, UPD, TH, AL> pw2;
   ParamBatch<1, UPD, TH, AL> pb1, pb2;
-  pw2.load(a, wrow, mrow, arow, idx_w2);
-  pb1.load(a, wrow, mrow, arow, idx_b1);
-  pb2.load(a, wrow, mrow, arow, idx_b2);
-  for (int i = t; i < h; i += kThreads) b1s[i] = wrow[ob1 + i];
-  if (t < c) b2s[t] = wrow[ob2 + t];
-  if (t < B) ys[t] = static_cast<int>(a.Y[int64_t(agent) * a.ldya + t]);
-  __syncthreads();
+  if constexpr (PH != 1) {
+    pw2.load(a, wrow, mrow, arow, idx_w2);
+    pb1.load(a, wrow, mrow, arow, idx_b1);
+    pb2.load(a, wrow, mrow, arow, idx_b2);
+    if (t < c) b2s[t] = wrow[ob2 + t];
+    if (t < B) ys[t] = static_cast<int>(a.Y[int64_t(agent) * a.ldya + t]);
+  }
+  if constexpr (PH == 0)
+    for (int i = t; i < h; i += kThreads) b1s[i] = wrow[ob1 + i];
+  if constexpr (PH != 1) __syncthreads();  // PH 1: the staging is the whole LDS (b1 read from memory below)
+  float* wsa = ws + int64_t(agent) * B * h;  // H (PH 1 -> 2), then dZ1 for mlp_dw1_kernel
+  if constexpr (PH == 2) {  // H from the F1 kernel
+    for (int o = t; o < B * h; o += kThreads) Hs[(o / h) * hp + (o % h)] = wsa[o];
+  } else {
 
   // ---- F1: Z1^T tiles (32 h x 32 b) on MFMA, K = d in chunks of 32
   const int nht = h / 32, nbt = (B + 31) / 32;
@@ -287,12 +299,16 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd_kernel(MlpArgs a, float* __r
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int hr = 32 * ht + (r & 3) + 8 * (r >> 2) + 4 * hh;
-          const float z = acc[u][r] + b1s[hr];
-          Hs[brow * hp + hr] = (z > 0.0f || z != z) ? z : 0.0f;  // relu, NaN propagates like torch
+          const float z = acc[u][r] + (PH == 1 ? wrow[ob1 + hr] : b1s[hr]);
+          const float hz = (z > 0.0f || z != z) ? z : 0.0f;  // relu, NaN propagates like torch
+          if constexpr (PH == 1) wsa[brow * h + hr] = hz;
+          else Hs[brow * hp + hr] = hz;
         }
       }
     }
   }
+  if constexpr (PH == 1) return;
+  }  // PH != 2
   for (int i = t; i < c * h; i += kThreads) W2s[(i / h) * hp + i % h] = wrow[oW2 + i];
   __syncthreads();
 
@@ -386,7 +402,6 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd_kernel(MlpArgs a, float* __r
   }
 
   // dZ1 for the W1 tiles of mlp_dw1_kernel
-  float* wsa = ws + int64_t(agent) * B * h;
   for (int o = t; o < B * h; o += kThreads) wsa[o] = Hs[(o / h) * hp + (o % h)];
   DOL_TRACE(3)
 }
@@ -537,6 +552,10 @@ extern "C" int dol_mlp_step_f32(float* w, int64_t ldw, float* grad, int64_t ldg,
   const dim3 grid(static_cast<unsigned>(n_agents)), block(kThreads);
   // F1 pipeline depth (DOL_MLP_STAGES = 2 / 3 / 4; diagnostics, default 3)
   static const int stages = [] { const char* e = getenv("DOL_MLP_STAGES"); return e ? atoi(e) : kStages; }();
+  // forward as two kernels (F1 / the per-agent tail; bit-identical), opt-in with
+  // DOL_MLP_SPLIT_FWD=1: measured 0.518-0.524 (F1 depth 3 / 4) and 0.509-0.511
+  // (depth 2) vs 0.509-0.513 ms fused (profiles/r03_mlp_split_fwd.txt)
+  static const int split_fwd = [] { const char* e = getenv("DOL_MLP_SPLIT_FWD"); return e ? atoi(e) : 0; }();
   const int upd = update ? mode + 1 : 0;
   float* ws = static_cast<float*>(work);
   const int64_t n_blk2 = int64_t((d + 31) / 32) * n_agents;
@@ -560,7 +579,20 @@ extern "C" int dol_mlp_step_f32(float* w, int64_t ldw, float* grad, int64_t ldg,
       return sizeof(float) * (fwd_union_floats(B, h, c, ns) + h + c + B) + sizeof(int) * size_t(B);
     };
     const bool nt1 = h * ((B + 31) / 32) <= 128;
-    if (stages == 2) {
+    if (split_fwd) {  // F1 kernel (staging only in LDS), then the per-agent tail kernel
+      auto f1 = [&](auto ns_c) {
+        constexpr int NS = decltype(ns_c)::value;
+        const size_t l1 = sizeof(float) * size_t(NS) * (h + 32 * ((B + 31) / 32)) * 32;
+        if (nt1) fwd(mlp_fwd_kernel<1, U, TH, AL, NS, 1>, l1);
+        else fwd(mlp_fwd_kernel<4, U, TH, AL, NS, 1>, l1);
+      };
+      if (stages == 2) f1(std::integral_constant<int, 2>{});
+      else if (stages == 4) f1(std::integral_constant<int, 4>{});
+      else if (stages == 5) f1(std::integral_constant<int, 5>{});
+      else f1(std::integral_constant<int, 3>{});
+      if (nt1) fwd(mlp_fwd_kernel<1, U, TH, AL, kStages, 2>, lds);
+      else fwd(mlp_fwd_kernel<4, U, TH, AL, kStages, 2>, lds);
+    } else if (stages == 2) {
       if (nt1) fwd(mlp_fwd_kernel<1, U, TH, AL, 2>, lds_for(2));
       else fwd(mlp_fwd_kernel<4, U, TH, AL, 2>, lds_for(2));
     } else if (stages == 4 && lds_for(4) <= 160 * 1024) {
