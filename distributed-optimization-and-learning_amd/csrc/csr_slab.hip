@@ -111,7 +111,8 @@ __device__ __forceinline__ uint32_t piece_addr(uint32_t o, uint32_t lb) { return
 // only (no gathers), 2 = no X staging (index blocks and gathers only), 3 = no
 // workgroup barrier per chunk (waves drift; reads race the DMA), 4 = no index
 // reads inside a row (every step reuses the row's first two pairs), 5 = the
-// products' multiplies dropped (acc += x: half the VALU).
+// products' multiplies dropped (acc += x: half the VALU), 6 = the tails (a
+// row's last np % 4 pairs) skipped.
 // Each row walks its chunk segment in groups of 4 / 2 / 1 entries: the index
 // pairs by uniform ds_read_b128 (segments are padded to even lengths, so two
 // entries share one 16-B LDS read: 2 LDS cycles per entry; ds_read2_b64 took
@@ -134,7 +135,7 @@ __device__ __forceinline__ uint32_t piece_addr(uint32_t o, uint32_t lb) { return
 // item.  Persistent (G < n_items): the chunk stream runs on across items — the
 // next item's chunk 0 is staged during the current item's last chunk, so a new
 // item does not start on an exposed DMA latency (needs nk >= 2).
-template <int PROBE = 0>
+template <int PROBE = 0, bool A4 = false>
 __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
     const float* __restrict__ X, int64_t ldx, int x_rows, float* __restrict__ Y, int64_t ldy, int n_rows, int64_t P,
     const int32_t* __restrict__ ent, const int32_t* __restrict__ hdr, int nk, int n_rg, int64_t n_slabs,
@@ -295,6 +296,15 @@ __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
           asm volatile("" : "+v"(a)::"memory");
           np -= 4;
         }
+        if constexpr (PROBE == 6) {  // diagnostics: a row's np % 4 tail pairs skipped
+          acc[r] = a;
+          continue;
+        }
+        if constexpr (A4) {  // np % 4 is 0 or 2 (segments of whole pairs of pairs)
+          if (np >= 2) a = step2(a, qa, qb);
+          acc[r] = a;
+          continue;
+        }
         if (np >= 2) {
           I4 na;
           if (np == 3) na = pair_at(ip);
@@ -432,7 +442,7 @@ __device__ __forceinline__ int lower_bound_col(const int32_t* __restrict__ col, 
 // hdr[g][k][i] <- number of row (g R + i)'s entries in chunk k (0 for i == R and rows past n_rows)
 __global__ __launch_bounds__(256) void slab_count_kernel(const int32_t* __restrict__ rowptr,
                                                          const int32_t* __restrict__ col, int n_rows, int nk,
-                                                         int64_t len, int32_t* __restrict__ hdr) {
+                                                         int64_t len, int32_t* __restrict__ hdr, int align) {
   const int64_t idx = int64_t(blockIdx.x) * 256 + threadIdx.x;
   if (idx >= len) return;
   const int i = int(idx % (kRows + 1));
@@ -445,7 +455,7 @@ __global__ __launch_bounds__(256) void slab_count_kernel(const int32_t* __restri
     const int lo = lower_bound_col(col, e0, e1, k * kChunk);
     c = lower_bound_col(col, lo, e1, (k + 1) * kChunk) - lo;
   }
-  hdr[idx] = c + (c & 1);  // segments padded to even lengths
+  hdr[idx] = (c + align - 1) / align * align;  // segments padded to a multiple of `align` (2 or 4)
 }
 
 // in-place exclusive scan of hdr[0..len) (one workgroup: a contiguous segment per thread)
@@ -596,7 +606,8 @@ __global__ __launch_bounds__(64) void slab_scatter_kernel(const int32_t* __restr
                                                           const int32_t* __restrict__ col,
                                                           const float* __restrict__ val, int nk,
                                                           const int32_t* __restrict__ inv,
-                                                          int32_t* __restrict__ hdr, int32_t* __restrict__ ent) {
+                                                          int32_t* __restrict__ hdr, int32_t* __restrict__ ent,
+                                                          int align) {
   const int r = blockIdx.x, g = r / kRows, i = inv[r];
   const int e0 = rowptr[r], e1 = rowptr[r + 1];
   for (int e = e0 + int(threadIdx.x); e < e1; e += 64) {
@@ -611,18 +622,28 @@ __global__ __launch_bounds__(64) void slab_scatter_kernel(const int32_t* __restr
   for (int k = int(threadIdx.x); k < nk; k += 64) {
     const int lo = lower_bound_col(col, e0, e1, k * kChunk);
     const int n = lower_bound_col(col, lo, e1, (k + 1) * kChunk) - lo;
-    if (n & 1) {
+    const int np = (n + align - 1) / align * align;
+    if (np > n) {
       int32_t* h = hdr + (int64_t(g) * nk + k) * (kRows + 1) + i;
-      const int64_t pad = *h + n;  // odd: the second slot of the segment's last pair
-      const int64_t q = (pad >> 1) * 4 + 2;  // (w1, off1) of the pair
-      ent[q] = 0;
-      ent[q + 1] = kZeroRel;
+      for (int64_t pad = *h + n; pad < *h + np; ++pad) {  // (0, zero piece) entries up to the alignment
+        const int64_t q = (pad >> 1) * 4 + 2 * (pad & 1);
+        ent[q] = 0;
+        ent[q + 1] = kZeroRel;
+      }
       *h |= 1;
     }
   }
 }
 
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// segment alignment of the packing and the kernel variant that reads it (one
+// value per process): 2 = pairs; 4 = pairs of pairs, so a row's tail is at most
+// one 2-pair step (DOL_SLAB_ALIGN)
+int slab_align() {
+  static const int a = [] { const char* e = getenv("DOL_SLAB_ALIGN"); return (e && atoi(e) == 4) ? 4 : 2; }();
+  return a;
+}
 
 }  // namespace
 
@@ -634,7 +655,7 @@ extern "C" int64_t dol_csr_slab_hdr_len(int32_t n_rows, int32_t x_rows) {
 }
 extern "C" int64_t dol_csr_slab_ent_len(int64_t nnz_cap, int32_t n_rows, int32_t x_rows) {
   if (nnz_cap < 0 || nnz_cap > dol::kMaxDim || n_rows < 0 || x_rows < 0) return 0;
-  return 2 * (nnz_cap + int64_t(n_rows) * dol_csr_slab_nk(x_rows) + kEntPad);  // + one pad per (row, chunk)
+  return 2 * (nnz_cap + 3 * int64_t(n_rows) * dol_csr_slab_nk(x_rows) + kEntPad);  // + <= 3 pads per (row, chunk)
 }
 
 extern "C" int dol_mix_csr_slab_f32(const float* X, int64_t ldx, int32_t x_rows, float* Y, int64_t ldy,
@@ -680,6 +701,8 @@ extern "C" int dol_mix_csr_slab_f32(const float* X, int64_t ldx, int32_t x_rows,
   else if (probe == 3) launch(csr_slab_kernel<3>);
   else if (probe == 4) launch(csr_slab_kernel<4>);
   else if (probe == 5) launch(csr_slab_kernel<5>);
+  else if (probe == 6) launch(csr_slab_kernel<6>);
+  else if (slab_align() == 4) launch(csr_slab_kernel<0, true>);
   else launch(csr_slab_kernel<0>);
   return dol::check_launch("dol_mix_csr_slab_f32");
 }
@@ -694,7 +717,7 @@ extern "C" int dol_csr_slab_pack(const int32_t* rowptr, const int32_t* col, cons
   const int64_t len = cdiv(n_rows, kRows) * nk * (kRows + 1);  // the header blocks
   if (cdiv(len, 256) >= (int64_t(1) << 31)) return fail(DOL_EINVAL, "dol_csr_slab_pack: too many chunk blocks");
   hipLaunchKernelGGL(slab_count_kernel, dim3(static_cast<unsigned>(cdiv(len, 256))), dim3(256), 0, s, rowptr, col,
-                     n_rows, nk, len, hdr);
+                     n_rows, nk, len, hdr, slab_align());
   const int64_t n_rg = cdiv(n_rows, kRows);
   const int64_t blocks = n_rg * nk * (kRows + 1);  // the header blocks; perm and inv follow
   int32_t* perm = hdr + blocks;
@@ -707,7 +730,7 @@ extern "C" int dol_csr_slab_pack(const int32_t* rowptr, const int32_t* col, cons
                      perm, inv, bal);
   hipLaunchKernelGGL(slab_scan_kernel, dim3(1), dim3(1024), 0, s, hdr, blocks);
   hipLaunchKernelGGL(slab_scatter_kernel, dim3(static_cast<unsigned>(n_rows)), dim3(64), 0, s, rowptr, col, val, nk,
-                     inv, hdr, ent);
+                     inv, hdr, ent, slab_align());
   return dol::check_launch("dol_csr_slab_pack");
 }
 

@@ -1475,12 +1475,17 @@ int dol_mix_ring_steps_f32(const float* X, int64_t ldx, float* Y, int64_t ldy, i
     const int64_t nrt = cdiv(n_rows, T);
     const int64_t grid = cdiv(nct, 8) * 8 * nrt;
     if (grid > kMaxBlocks) return fail(DOL_EINVAL, "dol_mix_ring_steps_f32: too large");
-    if (stream_nt)
-      hipLaunchKernelGGL((ring_stream_kernel<S, PF, true>), dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, s, X,
-                         ldx, Y, ldy, n_rows, nv, nct, w_prev, w_next, static_cast<uint32_t>(nrt), T);
-    else
-      hipLaunchKernelGGL((ring_stream_kernel<S, PF, false>), dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, s, X,
-                         ldx, Y, ldy, n_rows, nv, nct, w_prev, w_next, static_cast<uint32_t>(nrt), T);
+    // DOL_RING_STREAM_LDS (diagnostics): bytes of unused LDS per block, to cap
+    // the blocks per CU (the kernel itself uses none)
+    static const int pad_lds = [] { const char* e = getenv("DOL_RING_STREAM_LDS"); return e ? atoi(e) : 0; }();
+    auto go_k = [&](auto kern) {
+      if (pad_lds > 65536)
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, pad_lds);
+      hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(grid)), dim3(kThreads), pad_lds, s, X, ldx, Y, ldy, n_rows, nv,
+                         nct, w_prev, w_next, static_cast<uint32_t>(nrt), T);
+    };
+    if (stream_nt) go_k(ring_stream_kernel<S, PF, true>);
+    else go_k(ring_stream_kernel<S, PF, false>);
     return check_launch("dol_mix_ring_steps_f32");
   };
   auto go_stream = [&](auto steps_c, int T) {
