@@ -260,6 +260,104 @@ class ColumnSharded:
         return torch.cat(parts, dim=1)
 
 
+class AgentColumnTranspose:
+    """Config 5 across GPUs: per-agent nonlinear local steps AND a non-local W.
+
+    The local step (`BatchedMLP.step`, DIST/clients.py:34-59) needs whole agent
+    rows, so each rank r keeps its agents [lo_r, hi_r) agent-major (`rows`: an
+    [n_local, >=P] bank view).  The mix with an Erdos-Renyi / dense W needs
+    every agent, so `mix()` transposes the bank to parameter-column blocks with
+    one all_to_all (rank r receives columns column_bounds(P, world, r) of all N
+    agents, `cols`: [N, Pc_r]), mixes that block locally with the round's plan
+    (the same W on every rank: drawn from the shared seed; exact slab kernel;
+    no collective), and transposes back with a second all_to_all.  Per rank and
+    round that moves 2 (world-1)/world of its own rows' bytes -- against
+    (world-1) x that for an all_gather of X -- and every output element is the
+    same computation as on one GPU (bit-identical).  NCCL (= RCCL) exchanges
+    device tensors directly; gloo stages through host memory (rehearsal).
+
+    apply(X, Y, P=...): the column-block mix (default: the plan's HIP op; tests
+    inject a CPU checker)."""
+
+    def __init__(self, n_agents: int, P: int, device, group=None, apply=None):
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.N, self.P = n_agents, P
+        self.device = torch.device(device)
+        self.lo, self.hi = shard_bounds(n_agents, self.world, self.rank)
+        self.n_local = self.hi - self.lo
+        self.row_bounds = [shard_bounds(n_agents, self.world, q) for q in range(self.world)]
+        self.col_bounds = [column_bounds(P, self.world, q) for q in range(self.world)]
+        self.c0, self.c1 = self.col_bounds[self.rank]
+        self.Pc = self.c1 - self.c0
+        ldc = row_stride(max(self.Pc, 1))
+        self.cols = torch.empty(self.N, ldc, dtype=torch.float32, device=self.device)
+        self.cols_out = torch.empty_like(self.cols)
+        self._apply = apply
+        self.plan = None
+
+    def set_plan(self, plan) -> None:
+        if (plan.n_rows, plan.n_cols) != (self.N, self.N):
+            raise ValueError("AgentColumnTranspose.set_plan: W must be N x N")
+        self.plan = plan
+
+    def _staged(self) -> bool:
+        return self.device.type == "cuda" and dist.get_backend(self.group) == "gloo"
+
+    def _all_to_all(self, send: torch.Tensor, recv: torch.Tensor, send_splits, recv_splits) -> None:
+        if self._staged():
+            hs, hr = send.cpu(), torch.empty(recv.shape, dtype=recv.dtype)
+            dist.all_to_all_single(hr, hs, recv_splits, send_splits, group=self.group)
+            recv.copy_(hr)
+        else:
+            dist.all_to_all_single(recv, send, recv_splits, send_splits, group=self.group)
+
+    def to_columns(self, rows: torch.Tensor) -> None:
+        """rows [n_local, >=P] (this rank's agents) -> self.cols [N, Pc] (all agents, my columns)."""
+        P, n = self.P, self.n_local
+        if self.world == 1:
+            self.cols[:, :P].copy_(rows[:, :P])
+            return
+        send = torch.cat([rows[:, a:b].reshape(-1) for a, b in self.col_bounds])  # to rank q: my rows x its columns
+        recv = torch.empty(self.N * self.Pc, dtype=torch.float32, device=self.device)
+        self._all_to_all(send, recv, [n * (b - a) for a, b in self.col_bounds],
+                         [(h - l) * self.Pc for l, h in self.row_bounds])
+        # from rank q: its agents x my columns, in rank (= agent) order
+        self.cols[:, :self.Pc].copy_(recv.view(self.N, self.Pc))
+
+    def from_columns(self, rows: torch.Tensor) -> None:
+        """self.cols_out [N, Pc] -> rows [n_local, >=P] (this rank's agents, every column)."""
+        P, n = self.P, self.n_local
+        if self.world == 1:
+            rows[:, :P].copy_(self.cols_out[:, :P])
+            return
+        send = self.cols_out[:, :self.Pc].contiguous().view(-1)  # to rank q: its agents x my columns
+        recv = torch.empty(n * P, dtype=torch.float32, device=self.device)
+        self._all_to_all(send, recv, [(h - l) * self.Pc for l, h in self.row_bounds],
+                         [n * (b - a) for a, b in self.col_bounds])
+        off = 0
+        for a, b in self.col_bounds:  # from rank q: my agents x its columns
+            w = b - a
+            rows[:, a:b].copy_(recv[off:off + n * w].view(n, w))
+            off += n * w
+
+    def mix(self, rows: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """One Jacobi round Y = W X for this rank's agents (out may be rows' own
+        storage: the column block is a separate buffer)."""
+        out = rows if out is None else out
+        self.to_columns(rows)
+        if self.Pc > 0:
+            if self._apply is not None:
+                self._apply(self.cols, self.cols_out, P=self.Pc)
+            else:
+                if self.plan is None:
+                    raise RuntimeError("AgentColumnTranspose.mix: set_plan() first")
+                self.plan.apply(self.cols, self.cols_out, P=self.Pc)
+        self.from_columns(out)
+        return out
+
+
 def global_mean(local_rows: torch.Tensor, local_order: Sequence[int], m_total: int, P: int,
                 group=None, out: Optional[torch.Tensor] = None, ordered_sum=None) -> torch.Tensor:
     """'fast' global mean: local ordered partial sum, all_reduce(SUM), / m."""

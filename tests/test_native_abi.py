@@ -65,7 +65,7 @@ def test_slab_entry_points_check_arguments():
     fake = 1 << 20  # never dereferenced
     assert L.dol_csr_slab_nk(1024) == 16 and L.dol_csr_slab_nk(65) == 2 and L.dol_csr_slab_nk(0) == 0
     assert L.dol_csr_slab_hdr_len(1000, 1024) == 8 * 16 * 129 + 2 * 8 * 128  # blocks, perm, inv
-    assert L.dol_csr_slab_ent_len(100, 10, 130) == 2 * (100 + 10 * 3 + 160)
+    assert L.dol_csr_slab_ent_len(100, 10, 130) == 2 * (100 + 3 * 10 * 3 + 160)  # <= 3 pads per (row, chunk)
     rc = L.dol_mix_csr_slab_f32(fake, 16, 8, fake, 16, 8, 16, None, fake, None)
     assert rc == -1 and b"null pointer" in L.dol_last_error()
     rc = L.dol_mix_csr_slab_f32(fake, 16, 8, fake, 16, 8, 16, fake, fake, None)

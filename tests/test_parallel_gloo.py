@@ -285,3 +285,58 @@ def test_column_sharded_set_plan_keeps_injected_entries():
     sh.dgd_step(torch.zeros(6, sh.ld))
     sh.step()
     assert calls == ["checker", "checker", "b-dgd", "dgd-checker", "checker"]
+
+
+def _transpose_worker(rank, world, port, N, P, rounds, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rng = np.random.default_rng(21)
+        X = rng.standard_normal((N, P)).astype(np.float32)
+        tr = parallel.AgentColumnTranspose(N, P, "cpu")
+        rows = torch.from_numpy(np.ascontiguousarray(X[tr.lo:tr.hi]))
+        for k in range(rounds):  # a new W every round (config 5), the same on every rank
+            csr = _er_csr(N, 0.3, seed=100 + k)
+            tr._apply = cpu_apply_csr(csr)
+            rows.mul_(0.5).add_(0.25)  # a stand-in local step on the agent-major block
+            tr.mix(rows)
+        q.put((rank, tr.lo, rows.numpy().copy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def _er_csr(n, p, seed):
+    from dolhip import graph as G
+    r = np.random.default_rng(seed)
+    A = (r.random((n, n)) < p).astype(np.float32)
+    np.fill_diagonal(A, 0)
+    R = r.random((n, n)).astype(np.float32) * A
+    with np.errstate(invalid="ignore", divide="ignore"):
+        W = (R / R.sum(0, dtype=np.float32)).T.astype(np.float32)
+    return G.csr_from_dense(W)
+
+
+@pytest.mark.parametrize("world,N,P", [(2, 30, 300), (3, 25, 130), (4, 9, 70)])
+def test_agent_column_transpose_mix_matches_single_process(world, N, P):
+    """Config 5 across ranks (parallel.AgentColumnTranspose): agent-major blocks
+    for the local step, one all_to_all to parameter-column blocks, the mix with a
+    new W per round on every block, one all_to_all back -- bit-identical to one
+    process (uneven agent and column blocks, a rank with no columns at P = 70)."""
+    rounds = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_transpose_worker, args=(r, world, port, N, P, rounds, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    X = np.random.default_rng(21).standard_normal((N, P)).astype(np.float32)
+    for k in range(rounds):
+        c = _er_csr(N, 0.3, seed=100 + k)
+        X = ((X * np.float32(0.5)).astype(np.float32) + np.float32(0.25)).astype(np.float32)
+        X = oracle.mix_csr(X, c.rowptr, c.col, c.val)
+    assert oracle.bits_equal(np.concatenate([r[2] for r in res]), X)
