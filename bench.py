@@ -379,6 +379,57 @@ def er_exact_mix_round(device, N: int = 1024, P: int = 101770, reps: int = 10):
                     "W draw + device Neighbors + packing included in ms_per_round"}
 
 
+def config5_round_sharded(device, world: int, rank: int, N: int = 1024, reps: int = 10):
+    """Config 5 over `world` ranks (parallel.AgentColumnTranspose): each rank's
+    agent block takes the fused MLP step, then one all_to_all moves the bank to
+    parameter-column blocks, every rank mixes all N agents on its columns with
+    the round's W (drawn from the shared seed on every rank: no W traffic), and
+    one all_to_all moves it back.  Bit-identical to one GPU
+    (tests/test_parallel_gpu.py::test_config5_rounds_across_ranks_match_one_gpu).
+    Timed like the headline: barrier, max over ranks."""
+    from dolhip import graph as G, parallel
+    from dolhip.bank import AgentBank
+    from dolhip.mlp import BatchedMLP, mlp_layout
+    d, h, c, B = 784, 128, 10, 32
+    tr = parallel.AgentColumnTranspose(N, d * h + h + c * h + c, device)
+    bank = AgentBank(tr.n_local, mlp_layout(d, h, c), device)
+    mlp = BatchedMLP(bank, d, h, c)
+    gen = torch.Generator(device=device).manual_seed(2028 + rank)
+    bank.buffer("x").normal_(0, 0.05, generator=gen)
+    bank.buffer("mom", zero=True)
+    X = torch.empty(tr.n_local, B, d, device=device).normal_(generator=gen)
+    y = torch.randint(0, c, (tr.n_local, B), device=device, generator=gen)
+    Wbuf = torch.empty(N, N, device=device)
+    st = {"plan": None, "r": 0}
+
+    def one():
+        st["r"] += 1
+        mlp.step(X, y, lr=0.05, momentum=0.5, first_step=False)
+        W = G.erdos_renyi_stochastic_hip(N, 0.1, 2028 * 1000003 + st["r"], device, out=Wbuf)
+        st["plan"] = G.MixingPlan.from_dense(W, dense_kernel="csr", reuse=st["plan"])
+        tr.set_plan(st["plan"])
+        tr.mix(bank.rows())
+    for _ in range(2):
+        one()
+    torch.cuda.synchronize(device)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        one()
+    torch.cuda.synchronize(device)
+    dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=device)
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    el = float(el.item()) / reps
+    out = {"agents": N, "params": tr.P, "batch": B, "mlp": f"{d}-{h}-{c}", "ms_per_round": el * 1e3,
+           "rounds_per_s": 1.0 / el, "ranks": world, "agents_per_rank": tr.n_local, "columns_per_rank": tr.Pc,
+           "what": "config 5 over ranks: fused MLP step on each rank's agents, all_to_all to parameter-column "
+                   "blocks, bit-exact ER mix per block (same W on every rank), all_to_all back"}
+    del bank, mlp, X, y, Wbuf, st, tr
+    torch.cuda.empty_cache()
+    return out
+
+
 def config5_round(device, N: int = 1024, reps: int = 10):
     """Secondary (BASELINE config 5, N = 1): one whole round of the
     time-varying-graph MLP workload -- a new Erdos-Renyi p = 0.1 W drawn on the
@@ -549,8 +600,8 @@ def main():
         exact = er_exact_mix_round(device)
     _log("dense ER done")
     cfg5 = None
-    if world == 1 and not args.no_primal_dual:
-        cfg5 = config5_round(device)
+    if not args.no_primal_dual:
+        cfg5 = config5_round(device) if world == 1 else config5_round_sharded(device, world, rank)
     _log("config 5 round done")
 
     traffic = None
