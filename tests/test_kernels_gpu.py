@@ -607,6 +607,24 @@ def test_ring_steps_bit_identical_to_single_rounds(steps, n, P, gpu):
 
 
 @pytest.mark.parametrize("steps", [2, 5, 8])
+def test_ring_steps_interior_tiles(steps, gpu):
+    """ring_stream_kernel's interior path (1024-row tiles with every input row and
+    weight in range: here the tiles at rows 1024 and 2048 of 4096) next to the
+    wrap-around edge tiles, on a ragged column count."""
+    n, P = 4096, 1028
+    rng = np.random.default_rng(steps + 40)
+    X = rng.standard_normal((n, P)).astype(np.float32)
+    wp, wn = rng.random(n).astype(np.float32), rng.random(n).astype(np.float32)
+    want = X
+    for _ in range(steps):
+        want = oracle.mix_ring(want, wp, wn)
+    Y = torch.empty(n, P, device=gpu)
+    ops.mix_ring_steps(dev(X, gpu), Y, dev(wp, gpu), dev(wn, gpu), steps)
+    torch.cuda.synchronize()
+    assert bits_equal(Y.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("steps", [2, 5, 8])
 def test_ring_steps_signed_zeros_and_underflow(steps, gpu):
     """The fused pass's intermediate levels use fma(wp, a, +0) + wn*b, which may
     hold -0 where single rounds hold +0; the last level must still match the
