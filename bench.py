@@ -150,6 +150,17 @@ def cpu_baseline(sizes, P: int, seconds: float, full_agents: int):
         del W, X
     big = max(sizes)
     value = per_n[big]["rounds_per_s"] * big / full_agents
+    # the reference's round is O(N^2) in its Neighbors scan and O(N) in the
+    # consensus work: least-squares fit of seconds/round = a N^2 + b N over the
+    # samples, evaluated at full_agents (the per-byte `value` ignores the N^2 part)
+    fit = None
+    if len(sizes) >= 2:
+        A = np.array([[n * n, n] for n in sizes], dtype=np.float64)
+        t = np.array([1.0 / per_n[n]["rounds_per_s"] for n in sizes])
+        (a, b), *_ = np.linalg.lstsq(A, t, rcond=None)
+        t_full = a * full_agents ** 2 + b * full_agents
+        if t_full > 0:
+            fit = {"rounds_per_s": 1.0 / t_full, "seconds_per_round": t_full, "a_s_per_agent2": a, "b_s_per_agent": b}
     return {
         "value": value,
         "unit": "rounds/s",
@@ -158,6 +169,7 @@ def cpu_baseline(sizes, P: int, seconds: float, full_agents: int):
         "affinity_cpus": aff,
         "kind": "port",
         "per_agents": per_n,
+        "fit_a_n2_plus_b_n": fit,
         "vectorized": {"value": vec_n[big]["rounds_per_s"] * big / full_agents, "unit": "rounds/s", "cores": threads,
                        "kind": "port", "per_agents": vec_n,
                        "sample": "vectorized torch-CPU ring round (oracle/ref_cpu.py: roll + mul + add over the whole "
