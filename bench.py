@@ -584,7 +584,7 @@ def main():
         ms_pass = s_ev.elapsed_time(e_ev) / reps
         fedlcon = {"eps": eps, "rounds_per_s": eps * 1e3 / ms_pass, "ms_per_pass": ms_pass,
                    "GBps_per_pass": 2 * N * P * 4 / (ms_pass / 1e3) / 1e9,
-                   "what": "FedLCon eps=5 consensus rounds fused into one HBM pass (ring_stream_kernel: streaming temporal blocking), bit-identical"}
+                   "what": "FedLCon eps=5 consensus rounds fused into one HBM pass (ring_steps_kernel; DOL_RING_STREAM=1: the streaming variant), bit-identical"}
 
     # secondary (N = 1): config 3's random 4-regular mix at the headline size on
     # the parameter-major bank, in the headline's buffers

@@ -1457,14 +1457,16 @@ int dol_mix_ring_steps_f32(const float* X, int64_t ldx, float* Y, int64_t ldy, i
   if (steps == 0) return fail(DOL_EINVAL, "dol_mix_ring_steps_f32: steps must be >= 1");
   const bool vec = row_vec_ok(X, ldx) && row_vec_ok(Y, ldy) && P % 4 == 0;
   if (!vec || steps > 8) return fail(DOL_EINVAL, "dol_mix_ring_steps_f32: needs 16-B aligned rows, P %% 4 == 0 and steps <= 8 (compose launches otherwise)");
-  // ring_stream_kernel (1024-row tiles, 8 rows in flight, nontemporal loads)
-  // unless DOL_RING_STREAM=0 (the register-tile ring_steps_kernel).  eps = 5 at
-  // 8192 x 2^20, alternating on one box (profiles/r03_eps_stream.txt): box A
-  // stream 12.38 / 12.39 vs tiles 12.61 / 12.62 ms; box B stream-NT 11.60 /
-  // 12.00 / 11.76 vs tiles 11.90 / 11.92 / 11.80 (ring round 11.7-12.0 there):
-  // both at the ring round's rate, the clock 1 % below it (2424 / 2408 vs 2439
-  // MHz, GRBM_GUI_ACTIVE per XCD over the kernel's time).
-  static const int stream = [] { const char* e = getenv("DOL_RING_STREAM"); return e ? atoi(e) : 1; }();
+  // The register-tile ring_steps_kernel unless DOL_RING_STREAM=1
+  // (ring_stream_kernel: 1024-row tiles, 8 rows in flight, nontemporal loads).
+  // eps = 5 at 8192 x 2^20, alternating on one box (profiles/r03_eps_stream.txt):
+  // box A stream 12.38 / 12.39 vs tiles 12.61 / 12.62 ms; box C stream-NT 11.60 /
+  // 12.00 / 11.76 vs tiles 11.90 / 11.92 / 11.80; box E stream-NT 12.95-13.19 vs
+  // tiles 11.96-12.67; the stream kernel alone ran 10.66 ms on one box and 12.72
+  // on another with the same ring round (10.92 ms): no consistent winner, so the
+  // r02 default stays.  Clock 1 % below the ring kernel's for both (2424 / 2408
+  // vs 2439 MHz, GRBM_GUI_ACTIVE per XCD over the kernel's time).
+  static const int stream = [] { const char* e = getenv("DOL_RING_STREAM"); return e ? atoi(e) : 0; }();
   static const int stream_t = [] { const char* e = getenv("DOL_RING_STREAM_T"); return e ? atoi(e) : 1024; }();
   static const int stream_pf = [] { const char* e = getenv("DOL_RING_STREAM_PF"); return e ? atoi(e) : 8; }();
   static const int stream_nt = [] { const char* e = getenv("DOL_RING_STREAM_NT"); return e ? atoi(e) : 1; }();
