@@ -613,7 +613,14 @@ def main():
     _log("dense ER done")
     cfg5 = None
     if not args.no_primal_dual:
-        cfg5 = config5_round(device) if world == 1 else config5_round_sharded(device, world, rank)
+        if world == 1:
+            cfg5 = config5_round(device)
+        else:  # a secondary: an error here must not cost the headline line
+            try:
+                cfg5 = config5_round_sharded(device, world, rank)
+            except Exception as e:  # noqa: BLE001
+                cfg5 = {"error": f"{type(e).__name__}: {e}"[:300]}
+                _log(f"config-5 round over ranks failed: {cfg5['error']}")
     _log("config 5 round done")
 
     traffic = None
