@@ -392,52 +392,37 @@ def er_exact_mix_round(device, N: int = 1024, P: int = 101770, reps: int = 10):
 
 
 def config5_round_sharded(device, world: int, rank: int, N: int = 1024, reps: int = 10):
-    """Config 5 over `world` ranks (parallel.AgentColumnTranspose): each rank's
-    agent block takes the fused MLP step, then one all_to_all moves the bank to
-    parameter-column blocks, every rank mixes all N agents on its columns with
-    the round's W (drawn from the shared seed on every rank: no W traffic), and
-    one all_to_all moves it back.  Bit-identical to one GPU
+    """Config 5 over `world` ranks: dolhip.synthetic.TimeVaryingMLPGossip with
+    torch.distributed up -- each rank's agent block takes the fused MLP step,
+    one all_to_all moves the bank to parameter-column blocks, every rank mixes
+    all N agents on its columns with the round's W (drawn from the shared seed
+    on every rank, on a side stream during the local step), one all_to_all
+    moves it back.  Bit-identical to one GPU
     (tests/test_parallel_gpu.py::test_config5_rounds_across_ranks_match_one_gpu).
     Timed like the headline: barrier, max over ranks."""
-    from dolhip import graph as G, parallel
-    from dolhip.bank import AgentBank
-    from dolhip.mlp import BatchedMLP, mlp_layout
+    from dolhip.synthetic import TimeVaryingMLPGossip
     d, h, c, B = 784, 128, 10, 32
-    tr = parallel.AgentColumnTranspose(N, d * h + h + c * h + c, device)
-    bank = AgentBank(tr.n_local, mlp_layout(d, h, c), device)
-    mlp = BatchedMLP(bank, d, h, c)
+    sim = TimeVaryingMLPGossip(N, d, h, c, p_edge=0.1, lr=0.05, momentum=0.5, seed=2028, device=device)
     gen = torch.Generator(device=device).manual_seed(2028 + rank)
-    bank.buffer("x").normal_(0, 0.05, generator=gen)
-    bank.buffer("mom", zero=True)
-    X = torch.empty(tr.n_local, B, d, device=device).normal_(generator=gen)
-    y = torch.randint(0, c, (tr.n_local, B), device=device, generator=gen)
-    Wbuf = torch.empty(N, N, device=device)
-    st = {"plan": None, "r": 0}
-
-    def one():
-        st["r"] += 1
-        mlp.step(X, y, lr=0.05, momentum=0.5, first_step=False)
-        W = G.erdos_renyi_stochastic_hip(N, 0.1, 2028 * 1000003 + st["r"], device, out=Wbuf)
-        st["plan"] = G.MixingPlan.from_dense(W, dense_kernel="csr", reuse=st["plan"])
-        tr.set_plan(st["plan"])
-        tr.mix(bank.rows())
+    sim.batch(torch.empty(sim.n_local, B, d, device=device).normal_(generator=gen),
+              torch.randint(0, c, (sim.n_local, B), device=device, generator=gen))
     for _ in range(2):
-        one()
+        sim.round()
     torch.cuda.synchronize(device)
     dist.barrier()
     t0 = time.perf_counter()
     for _ in range(reps):
-        one()
+        sim.round()
     torch.cuda.synchronize(device)
     dist.barrier()
     el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=device)
     dist.all_reduce(el, op=dist.ReduceOp.MAX)
     el = float(el.item()) / reps
-    out = {"agents": N, "params": tr.P, "batch": B, "mlp": f"{d}-{h}-{c}", "ms_per_round": el * 1e3,
-           "rounds_per_s": 1.0 / el, "ranks": world, "agents_per_rank": tr.n_local, "columns_per_rank": tr.Pc,
-           "what": "config 5 over ranks: fused MLP step on each rank's agents, all_to_all to parameter-column "
-                   "blocks, bit-exact ER mix per block (same W on every rank), all_to_all back"}
-    del bank, mlp, X, y, Wbuf, st, tr
+    out = {"agents": N, "params": sim.P, "batch": B, "mlp": f"{d}-{h}-{c}", "ms_per_round": el * 1e3,
+           "rounds_per_s": 1.0 / el, "ranks": world, "agents_per_rank": sim.n_local, "columns_per_rank": sim.tr.Pc,
+           "what": "config 5 over ranks (TimeVaryingMLPGossip): fused MLP step on each rank's agents, all_to_all to "
+                   "parameter-column blocks, bit-exact ER mix per block (same W on every rank), all_to_all back"}
+    del sim
     torch.cuda.empty_cache()
     return out
 
@@ -487,15 +472,32 @@ def config5_round(device, N: int = 1024, reps: int = 10):
     for k in range(reps):
         one(k)
     torch.cuda.synchronize(device)
-    el = (time.perf_counter() - t0) / reps
+    el_seq = (time.perf_counter() - t0) / reps
     ms = {k: sum(a.elapsed_time(b) for a, b in v) / reps for k, v in ev.items()}
     P = bank.P
+    del bank, mlp, Wbuf, st
+    torch.cuda.empty_cache()
+    # the product path: dolhip.synthetic.TimeVaryingMLPGossip, the W draw + CSR
+    # build on a side stream during the local step
+    from dolhip.synthetic import TimeVaryingMLPGossip
+    sim = TimeVaryingMLPGossip(N, d, h, c, p_edge=0.1, lr=0.05, momentum=0.5, seed=2028, device=device)
+    sim.batch(X, y)
+    for _ in range(2):
+        sim.round()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        sim.round()
+    torch.cuda.synchronize(device)
+    el = (time.perf_counter() - t0) / reps
+    del sim
     out = {"agents": N, "params": P, "batch": B, "mlp": f"{d}-{h}-{c}", "ms_per_round": el * 1e3,
-           "rounds_per_s": 1.0 / el, "phase_ms": ms,
+           "rounds_per_s": 1.0 / el, "ms_per_round_sequential": el_seq * 1e3, "phase_ms": ms,
            "local_GBps": N * (4 * P + B * d) * 4 / (ms["local"] / 1e3) / 1e9,
-           "what": "config 5 round: ER p=0.1 W drawn on device + device Neighbors/packing, fused MLP local step "
-                   "(momentum SGD) on fp32 MFMA, bit-exact LDS-gather CSR mix of the parameter rows"}
-    del bank, mlp, X, y, Wbuf, st
+           "what": "config 5 round (dolhip.synthetic.TimeVaryingMLPGossip): ER p=0.1 W drawn on device + device "
+                   "Neighbors/packing on a side stream, fused MLP local step (momentum SGD) on fp32 MFMA, bit-exact "
+                   "LDS-gather CSR mix of the parameter rows; phase_ms from the same round run sequentially"}
+    del X, y
     torch.cuda.empty_cache()
     return out
 

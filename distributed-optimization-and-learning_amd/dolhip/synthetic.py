@@ -309,3 +309,85 @@ class SeparableDGDPM:
     def consensus_error(self) -> float:
         x = self.XT[:, :self.N]
         return float((x - x.mean(1, keepdim=True)).norm() / max(1, self.N) ** 0.5)
+
+
+class TimeVaryingMLPGossip:
+    """BASELINE config 5 as a first-class round: N agents, each an
+    nn.Sequential(Linear(d, h), ReLU(), Linear(h, c)) row of the bank, a new
+    Erdos-Renyi p W drawn every round ('stochastic' weighting,
+    DIST/simulators.py:65-70), one local momentum-SGD step per agent on its
+    batch (DIST/clients.py:34-59: forward, CrossEntropyLoss, backward, step;
+    the fused dol_mlp_step_f32), then the synchronous consensus round with that
+    W (DIST/clients.py:61-69, bit-exact: device Neighbors + the LDS-gather CSR
+    kernel).  One process per GPU: with torch.distributed initialised, rank r
+    owns the agent block shard_bounds(N, world, r) and the mix runs through
+    parallel.AgentColumnTranspose (bit-identical to one GPU).  The round's W
+    draw + CSR build runs on a side stream, overlapped with the local step.
+
+    batch(X, y): per-agent batches for this rank's agents ([n_local, B, d] float32,
+    [n_local, B] int64), kept until replaced."""
+
+    def __init__(self, n_agents: int, d: int = 784, h: int = 128, c: int = 10, p_edge: float = 0.1,
+                 lr: float = 0.05, momentum: float = 0.5, seed: int = 2028, device=None, group=None,
+                 init_std: float = 0.05):
+        import torch.distributed as dist
+        from . import parallel
+        from .mlp import BatchedMLP, mlp_layout
+        self.N, self.d, self.h, self.c = int(n_agents), d, h, c
+        self.p_edge, self.lr, self.mu, self.seed = float(p_edge), float(lr), float(momentum), int(seed)
+        self.device = torch.device("cuda" if device is None else device)
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.lo, self.hi = parallel.shard_bounds(self.N, self.world, self.rank)
+        self.n_local = self.hi - self.lo
+        self.bank = AgentBank(self.n_local, mlp_layout(d, h, c), self.device)
+        self.P = self.bank.P
+        self.mlp = BatchedMLP(self.bank, d, h, c)
+        # every agent's initial row from one global stream: the same model whatever the sharding
+        g = torch.Generator(device=self.device).manual_seed(self.seed)
+        full = torch.empty(self.N, self.P, device=self.device).normal_(0, init_std, generator=g)
+        self.bank.rows()[:] = full[self.lo:self.hi]
+        del full
+        self.bank.buffer("y").zero_()
+        if self.mu != 0.0:
+            self.bank.buffer("mom", zero=True)
+        self.tr = parallel.AgentColumnTranspose(self.N, self.P, self.device, group) if self.world > 1 else None
+        self._W = torch.empty(self.N, self.N, device=self.device)
+        self._plan = None
+        self._side = torch.cuda.Stream(self.device)
+        self.X = self.y = None
+        self.rounds = 0
+        self.losses = []
+
+    def batch(self, X: torch.Tensor, y: torch.Tensor) -> None:
+        if X.shape[:1] != (self.n_local,) or y.shape[:1] != (self.n_local,) or X.shape[-1] != self.d:
+            raise ValueError(f"batch: expected X [{self.n_local}, B, {self.d}] and y [{self.n_local}, B]")
+        self.X, self.y = X, y
+
+    def round_seed(self, r: int) -> int:
+        return self.seed * 1000003 + r + 1
+
+    def round(self) -> torch.Tensor:
+        """One round; returns this rank's per-agent losses (device tensor)."""
+        from . import graph as G
+        if self.X is None:
+            raise RuntimeError("TimeVaryingMLPGossip.round: call batch() first")
+        main = torch.cuda.current_stream(self.device)
+        self._side.wait_stream(main)  # the previous round's mix has consumed the old plan
+        with torch.cuda.stream(self._side):
+            W = G.erdos_renyi_stochastic_hip(self.N, self.p_edge, self.round_seed(self.rounds), self.device,
+                                             out=self._W)
+            self._plan = G.MixingPlan.from_dense(W, dense_kernel="csr", reuse=self._plan)
+        loss = self.mlp.step(self.X, self.y, lr=self.lr, momentum=self.mu, first_step=(self.rounds == 0))
+        main.wait_stream(self._side)
+        if self.tr is None:
+            self.bank.mix(self._plan)
+        else:
+            self.tr.set_plan(self._plan)
+            self.tr.mix(self.bank.rows())
+        self.rounds += 1
+        self.losses.append(loss)
+        return loss
+
+    def params(self) -> torch.Tensor:
+        return self.bank.rows()

@@ -357,29 +357,11 @@ def _config5_worker(rank, world, port, N, rounds, q):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, os.path.join(root, "distributed-optimization-and-learning_amd"))
-    from dolhip import graph as G, parallel
-    from dolhip.bank import AgentBank
-    from dolhip.mlp import BatchedMLP, mlp_layout
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        dev = torch.device("cuda:0")
-        x0, Xb, yb = _config5_data(N, dev)
-        tr = parallel.AgentColumnTranspose(N, x0.shape[1], dev)
-        bank = AgentBank(tr.n_local, mlp_layout(*_C5), dev)
-        mlp = BatchedMLP(bank, *_C5)
-        bank.rows()[:] = x0[tr.lo:tr.hi]
-        bank.buffer("mom", zero=True)
-        plan = None
-        for k in range(rounds):
-            mlp.step(Xb[tr.lo:tr.hi], yb[tr.lo:tr.hi], lr=0.05, momentum=0.5, first_step=(k == 0))
-            W = G.erdos_renyi_stochastic_hip(N, 0.1, 3000 + k, dev)  # the same W on every rank
-            plan = G.MixingPlan.from_dense(W, dense_kernel="csr", reuse=plan)
-            tr.set_plan(plan)
-            tr.mix(bank.rows())
-        torch.cuda.synchronize()
-        q.put((rank, bank.rows().cpu().numpy()))
+        q.put((rank, _config5_sim(N, rounds, torch.device("cuda:0"))))
     finally:
         dist.destroy_process_group()
 
@@ -387,50 +369,69 @@ def _config5_worker(rank, world, port, N, rounds, q):
 _C5 = (784, 32, 10)  # d, h, c (a narrower hidden layer than bench's 128 keeps the test quick)
 
 
-def _config5_data(N, dev):
-    d, h, c = _C5
-    P = d * h + h + c * h + c  # Linear(d, h), Linear(h, c) in state_dict order
+def _config5_batch(N, dev):
     g = torch.Generator(device=dev).manual_seed(77)
-    x0 = torch.empty(N, P, device=dev).normal_(0, 0.05, generator=g)
-    Xb = torch.empty(N, 8, _C5[0], device=dev).normal_(generator=g)
-    yb = torch.randint(0, _C5[2], (N, 8), device=dev, generator=g)
-    return x0, Xb, yb
+    return (torch.empty(N, 8, _C5[0], device=dev).normal_(generator=g),
+            torch.randint(0, _C5[2], (N, 8), device=dev, generator=g))
 
 
-@pytest.mark.parametrize("world,N", [(2, 70), (3, 130)])
-def test_config5_rounds_across_ranks_match_one_gpu(world, N, gpu):
-    """BASELINE config 5 across ranks (parallel.AgentColumnTranspose): the fused
-    MLP local step on each rank's agent block, a new Erdos-Renyi W per round
-    (device draw + device Neighbors, the same on every rank), the exact mix on
-    parameter-column blocks between two all_to_alls -- bit-identical to one
-    process running the same rounds (DIST/clients.py:34-69)."""
+def _config5_sim(N, rounds, dev):
+    """dolhip.synthetic.TimeVaryingMLPGossip for `rounds` rounds on this rank."""
+    from dolhip.synthetic import TimeVaryingMLPGossip
+    sim = TimeVaryingMLPGossip(N, *_C5, p_edge=0.1, lr=0.05, momentum=0.5, seed=31, device=dev)
+    Xb, yb = _config5_batch(N, dev)
+    sim.batch(Xb[sim.lo:sim.hi].contiguous(), yb[sim.lo:sim.hi].contiguous())
+    for _ in range(rounds):
+        sim.round()
+    torch.cuda.synchronize()
+    return sim.params().cpu().numpy()
+
+
+def _config5_by_hand(N, rounds, dev):
+    """The same rounds assembled from the parts on one GPU: AgentBank + the fused
+    MLP step + MixingPlan.from_dense(W, 'csr') + bank.mix."""
     from dolhip import graph as G
     from dolhip.bank import AgentBank
     from dolhip.mlp import BatchedMLP, mlp_layout
-    rounds = 3
-    x0, Xb, yb = _config5_data(N, gpu)
-    bank = AgentBank(N, mlp_layout(*_C5), gpu)
+    bank = AgentBank(N, mlp_layout(*_C5), dev)
     mlp = BatchedMLP(bank, *_C5)
-    bank.rows()[:] = x0
+    g = torch.Generator(device=dev).manual_seed(31)
+    bank.rows()[:] = torch.empty(N, bank.P, device=dev).normal_(0, 0.05, generator=g)
     bank.buffer("mom", zero=True)
     bank.buffer("y").zero_()
+    Xb, yb = _config5_batch(N, dev)
     plan = None
     for k in range(rounds):
-        mlp.step(Xb, yb, lr=0.05, momentum=0.5, first_step=(k == 0))
-        W = G.erdos_renyi_stochastic_hip(N, 0.1, 3000 + k, gpu)
+        W = G.erdos_renyi_stochastic_hip(N, 0.1, 31 * 1000003 + k + 1, dev)
         plan = G.MixingPlan.from_dense(W, dense_kernel="csr", reuse=plan)
+        mlp.step(Xb, yb, lr=0.05, momentum=0.5, first_step=(k == 0))
         bank.mix(plan)
     torch.cuda.synchronize()
-    want = bank.rows().cpu().numpy()
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_config5_worker, args=(r, world, port, N, rounds, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda t: t[0])
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
+    return bank.rows().cpu().numpy()
+
+
+@pytest.mark.parametrize("world,N", [(1, 70), (2, 70), (3, 130)])
+def test_config5_rounds_across_ranks_match_one_gpu(world, N, gpu):
+    """BASELINE config 5 (dolhip.synthetic.TimeVaryingMLPGossip): the fused MLP
+    local step on each rank's agent block, a new Erdos-Renyi W per round (device
+    draw + device Neighbors on a side stream, the same on every rank), the exact
+    mix on parameter-column blocks between two all_to_alls -- bit-identical to
+    the rounds assembled by hand on one GPU (DIST/clients.py:34-69)."""
     import oracle
-    assert oracle.bits_equal(np.concatenate([r[1] for r in res]), want)
+    rounds = 3
+    want = _config5_by_hand(N, rounds, gpu)
+    if world == 1:
+        got = _config5_sim(N, rounds, gpu)
+    else:
+        ctx = mp.get_context("spawn")
+        q = ctx.Queue()
+        port = _free_port()
+        procs = [ctx.Process(target=_config5_worker, args=(r, world, port, N, rounds, q)) for r in range(world)]
+        for p in procs:
+            p.start()
+        res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda t: t[0])
+        for p in procs:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+        got = np.concatenate([r[1] for r in res])
+    assert oracle.bits_equal(got, want)
