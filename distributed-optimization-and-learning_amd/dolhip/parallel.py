@@ -296,6 +296,10 @@ class AgentColumnTranspose:
         self.cols_out = torch.empty_like(self.cols)
         self._apply = apply
         self.plan = None
+        # exchange buffers, allocated once (the same sizes every round): rows ->
+        # columns sends n_local x P and receives N x Pc floats, and back
+        self._buf_rows = torch.empty(max(self.n_local * P, 1), dtype=torch.float32, device=self.device)
+        self._buf_cols = torch.empty(max(self.N * self.Pc, 1), dtype=torch.float32, device=self.device)
 
     def set_plan(self, plan) -> None:
         if (plan.n_rows, plan.n_cols) != (self.N, self.N):
@@ -319,8 +323,12 @@ class AgentColumnTranspose:
         if self.world == 1:
             self.cols[:, :P].copy_(rows[:, :P])
             return
-        send = torch.cat([rows[:, a:b].reshape(-1) for a, b in self.col_bounds])  # to rank q: my rows x its columns
-        recv = torch.empty(self.N * self.Pc, dtype=torch.float32, device=self.device)
+        send = self._buf_rows[:n * P]
+        off = 0
+        for a, b in self.col_bounds:  # to rank q: my rows x its columns
+            send[off:off + n * (b - a)].view(n, b - a).copy_(rows[:, a:b])
+            off += n * (b - a)
+        recv = self._buf_cols[:self.N * self.Pc]
         self._all_to_all(send, recv, [n * (b - a) for a, b in self.col_bounds],
                          [(h - l) * self.Pc for l, h in self.row_bounds])
         # from rank q: its agents x my columns, in rank (= agent) order
@@ -332,8 +340,9 @@ class AgentColumnTranspose:
         if self.world == 1:
             rows[:, :P].copy_(self.cols_out[:, :P])
             return
-        send = self.cols_out[:, :self.Pc].contiguous().view(-1)  # to rank q: its agents x my columns
-        recv = torch.empty(n * P, dtype=torch.float32, device=self.device)
+        send = self._buf_cols[:self.N * self.Pc]
+        send.view(self.N, self.Pc).copy_(self.cols_out[:, :self.Pc])  # to rank q: its agents x my columns
+        recv = self._buf_rows[:n * P]
         self._all_to_all(send, recv, [(h - l) * self.Pc for l, h in self.row_bounds],
                          [n * (b - a) for a, b in self.col_bounds])
         off = 0
