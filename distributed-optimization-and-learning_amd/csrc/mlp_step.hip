@@ -151,8 +151,9 @@ struct ParamBatch {
 __device__ __forceinline__ void wait_vmcnt(int n) {
   switch (n) {
 #define DOL_VMC(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
-    DOL_VMC(0) DOL_VMC(1) DOL_VMC(2) DOL_VMC(3) DOL_VMC(4) DOL_VMC(5) DOL_VMC(6) DOL_VMC(7)
-    DOL_VMC(8) DOL_VMC(9) DOL_VMC(10) DOL_VMC(11) DOL_VMC(12) DOL_VMC(13) DOL_VMC(14) DOL_VMC(15)
+#define DOL_VMC8(N) DOL_VMC(N) DOL_VMC(N + 1) DOL_VMC(N + 2) DOL_VMC(N + 3) DOL_VMC(N + 4) DOL_VMC(N + 5) DOL_VMC(N + 6) DOL_VMC(N + 7)
+    DOL_VMC8(0) DOL_VMC8(8) DOL_VMC8(16) DOL_VMC8(24) DOL_VMC8(32) DOL_VMC8(40) DOL_VMC8(48) DOL_VMC8(56)
+#undef DOL_VMC8
 #undef DOL_VMC
     default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
   }
@@ -160,12 +161,132 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
 
 constexpr int kStages = 3;  // default F1 LDS-DMA pipeline depth (NS - 1 chunks in flight during the MFMAs)
 
-// LDS layout of mlp_fwd_kernel (floats): [ union: F1 staging | Hs, W2s, Zs ] [ b1s, b2s, ls ] [ ys ]
-__host__ __device__ inline int64_t fwd_union_floats(int B, int h, int c, int ns = kStages) {
-  const int64_t Bp = 32 * ((B + 31) / 32);
-  const int64_t staging = int64_t(ns) * (h + Bp) * 32;
+// LDS layout of mlp_fwd_kernel (floats): [ union: F1 staging | Hs, W2s, Zs ] [ b1s, b2s, ls ] [ ys ];
+// the fused kernel (PH 3) keeps them apart: [ staging ] [ Hs, W2s, Zs ] [ ... ]
+__host__ __device__ inline int64_t fwd_staging_floats(int B, int h, int ns) {
+  return int64_t(ns) * (h + 32 * ((B + 31) / 32)) * 32;
+}
+// PH 3: W1 chunks parked in LDS instead of registers (the last KL of NK; 16 KiB each)
+__host__ __device__ constexpr int fused_park_chunks(int nk, int ns) { return nk <= 8 ? 0 : ns <= 4 ? 3 : ns == 5 ? 2 : 0; }
+__host__ __device__ inline int64_t fwd_union_floats(int B, int h, int c, int ns = kStages, bool fused = false,
+                                                    int park = 0) {
+  const int64_t staging = fwd_staging_floats(B, h, ns);
   const int64_t post = int64_t(B) * (h + 4) + int64_t(c) * (h + 4) + int64_t(B) * c;
-  return staging > post ? staging : post;
+  return fused ? staging + 4096 * int64_t(park) + post : staging > post ? staging : post;
+}
+
+// Buffer-descriptor memory ops (mlp_fused_dw1, mlp_dw1_kernel): dead lanes
+// point out of range (loads return 0, stores are dropped).
+using rsrc_t = __amdgpu_buffer_rsrc_t;
+constexpr uint32_t kOOB = 0x80000000u;  // any lane offset >= every buffer's size
+
+__device__ __forceinline__ rsrc_t make_rsrc(const float* p, int64_t nbytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), 0, static_cast<int>(nbytes), 0x00020000);
+}
+__device__ __forceinline__ float bload(rsrc_t r, uint32_t voff, uint32_t soff) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, static_cast<int>(voff), static_cast<int>(soff), 0));
+}
+__device__ __forceinline__ void bstore_nt(rsrc_t r, uint32_t voff, uint32_t soff, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, static_cast<int>(voff), static_cast<int>(soff), 2);
+}
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+// plain (write-back) 16-B stores: each one writes two 16-B pieces of 32 rows, and
+// the nontemporal hint on that pattern made the B1 phase 4x slower (261 vs 66 us
+// per agent, tools/mlp_phase.hip) -- the partial lines must merge in L2
+__device__ __forceinline__ void bstore4(rsrc_t r, uint32_t voff, f4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, static_cast<int>(voff), 0, 0);
+}
+
+// B1 + the W1 update of the fused step (mlp_fwd_kernel PH 3), on the W1 that
+// F1 left in registers.  Per 32-column chunk dt: the dW1^T tile [32 d x 32 h] =
+// X^T dZ1 on MFMA (K = B), with the tile's d rows permuted -- A row i holds
+// column sigma(i) = 16 ((i >> 2) & 1) + 4 (i >> 3) + (i & 3) -- so accumulator
+// r = 4 j + q of lane (li, hh) is the gradient of W1[32 wave + li][32 dt + 16 hh +
+// 4 j + q] = wres[dt][j][q]: exactly where F1 left that weight.  The products
+// and their k order are those of mlp_dw1_kernel with A and B swapped (two
+// chains, even / odd k-steps): bit-identical.  Momentum and X chunks stream
+// through the F1 staging ring (LDS-DMA, NS deep; the first NS - 1 were issued
+// before F2 and landed during F2 .. B2).  W1 / momentum / gradient tiles go out
+// as 16-B buffer stores that are always issued (masked lanes point out of
+// range, absent buffers have size 0), so the per-chunk vmcnt below can count
+// them: vector memory ops retire in issue order on gfx9, loads and stores alike.
+template <int UPD, int NS, int NK, int KL, class Issue>
+__device__ __forceinline__ void mlp_fused_dw1(const MlpArgs& a, const f4 (&wres)[NK - KL][4], const float* park, const float* Hs,
+                                              const float* stg, int rows, float* wrow, float* grow, float* mrow,
+                                              Issue& issue, int i0, int ipw) {
+  const int B = a.B, d = a.d, h = a.h;
+  const int hp = h + 4;
+  int lane = threadIdx.x & 63;
+  asm volatile("" : "+v"(lane));  // fresh lane-derived addresses: no CSE with F1's, held live across it
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int li = lane & 31, hh = lane >> 5;
+  const int64_t P = int64_t(h) * d + h + int64_t(a.c) * h + a.c;
+  const rsrc_t rW = make_rsrc(wrow, P * 4);
+  const rsrc_t rM = make_rsrc(UPD >= 2 ? mrow : wrow, UPD >= 2 ? P * 4 : 0);
+  const rsrc_t rG = make_rsrc(grow ? grow : wrow, grow ? P * 4 : 0);
+  float bz[16];  // B operand: dZ1[b = 2 s + hh][32 wave + li]
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    const int b = 2 * s + hh;
+    const float v = Hs[min(b, B - 1) * hp + 32 * wave + li];  // unconditional read, then select (no branch)
+    bz[s] = b < B ? v : 0.f;
+  }
+  const int sg = 16 * ((li >> 2) & 1) + 4 * (li >> 3) + (li & 3);  // sigma(li)
+  const int xp = sg >> 2, xe = sg & 3;                               // its 16-B piece, element
+  const int ipw_b1 = ipw - i0;                                       // DMA instructions per wave per chunk
+  constexpr int kSt = 12;                                            // 16-B stores per lane per tile
+  const uint32_t rowoff = uint32_t(((32 * wave + li) * d + 16 * hh) * 4);
+#pragma unroll
+  for (int dt = 0; dt < NK; ++dt) {
+    // ops issued after chunk dt's DMA: the next chunks' DMAs and the last tiles' stores
+    const int later = min(NS - 2, NK - 1 - dt) * ipw_b1 + min(dt, NS - 1) * kSt;
+    wait_vmcnt(min(later, 63));
+    __builtin_amdgcn_s_barrier();  // chunk dt landed for every wave; stage (dt - 1) % NS is free
+    if (dt + NS - 1 < NK) issue(dt + NS - 1, mrow, i0);
+    const float* st = stg + (dt % NS) * rows * 32;
+    float xv[16];  // A operand: X[b = 2 s + hh][32 dt + sigma(li)]
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int b = 2 * s + hh;  // < 32: always inside the staged X rows
+      const float v = st[(h + b) * 32 + ((xp ^ (b & 7)) * 4) + xe];
+      xv[s] = b < B ? v : 0.f;
+    }
+    f32x16 acc, acc1;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = acc1[r] = 0.f;
+#pragma unroll
+    for (int s = 0; s < 16; s += 2) {
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xv[s], bz[s], acc, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(xv[s + 1], bz[s + 1], acc1, 0, 0, 0);
+    }
+    acc += acc1;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      f4 mv = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (UPD == 3) mv = *reinterpret_cast<const f4*>(st + (32 * wave + li) * 32 + ((4 * hh + j) ^ (li & 7)) * 4);
+      const f4 w0 = dt < NK - KL ? wres[dt < NK - KL ? dt : 0][j]
+                                 : *reinterpret_cast<const f4*>(park + ((dt - (NK - KL)) * 16 + wave * 4 + j) * 256 + lane * 4);
+      f4 g, w, m;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float gg = acc[4 * j + q];
+        float dd = gg, mr = 0.f;
+        if constexpr (UPD == 2) {
+          mr = gg;
+        } else if constexpr (UPD == 3) {
+          mr = mv[q] * a.mom + gg;
+          dd = mr;
+        }
+        g[q] = gg;
+        m[q] = mr;
+        w[q] = __builtin_fmaf(a.neg_lr, dd, w0[q]);
+      }
+      const uint32_t vo = 32 * dt + 16 * hh + 4 * j < d ? rowoff + uint32_t((32 * dt + 4 * j) * 4) : kOOB;
+      bstore4(rG, vo, g);
+      bstore4(rW, vo, w);
+      bstore4(rM, vo, m);
+    }
+  }
 }
 
 // Per-agent part: forward, CE, backward down to dZ1 (-> ws[agent][b][h]),
@@ -181,15 +302,25 @@ __host__ __device__ inline int64_t fwd_union_floats(int B, int h, int c, int ns 
 // (F2, CE, B2, dZ1 -> ws) from that H.  1 + 2 run the same operations in the
 // same order as 0 (bit-identical); the split lets F1 stream W1 without the
 // HBM-idle tail and with deeper staging.
-template <int NT, int UPD, bool TH, bool AL, int NS = kStages, int PH = 0>
+// PH 3 (r03): the whole step in one kernel for h = 128, B <= 32 and NK = d / 32
+// chunks known at compile time -- F1 keeps every W1 fragment it reads (NK x 16
+// floats per lane: the agent's 128 x d W1 lives in the CU's register file), so
+// B1 + the W1 update run on the resident W1 and W1 is read from HBM once, not
+// twice; see mlp_fused_dw1 above.  Bit-identical to 0 + mlp_dw1_kernel
+// (tests/test_mlp_gpu.py::test_fused_one_kernel_step_bit_identical), opt-in
+// (DOL_MLP_FUSED=1): see the measurement at the dispatch below.
+template <int NT, int UPD, bool TH, bool AL, int NS = kStages, int PH = 0, int NK = 0>
 __global__ __launch_bounds__(kThreads) void mlp_fwd_kernel(MlpArgs a, float* __restrict__ ws) {
+  static_assert(PH != 3 || (NT == 1 && NK > 0 && !TH && !AL && UPD >= 1), "fused step: plain / momentum SGD, one tile per wave");
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int B = a.B, d = a.d, h = a.h, c = a.c;
   const int hp = h + 4;  // padded LDS rows: 16-B aligned, rows 4 banks apart
-  float* Hs = lds;                   // [B][hp]  H, later dZ1   (after F1)
+  constexpr int KL = PH == 3 ? fused_park_chunks(NK, NS) : 0;
+  float* park = lds + fwd_staging_floats(B, h, NS);  // PH 3: [KL][4 waves][4 j][64 lanes] f4
+  float* Hs = lds + (PH == 3 ? fwd_staging_floats(B, h, NS) + 4096 * KL : 0);  // [B][hp]  H, later dZ1   (after F1)
   float* W2s = Hs + B * hp;          // [c][hp]                 (after F1)
   float* Zs = W2s + c * hp;          // [B][c]   Z2, later dZ2
-  float* b1s = lds + fwd_union_floats(B, h, c, NS);  // [h]
+  float* b1s = lds + fwd_union_floats(B, h, c, NS, PH == 3, KL);  // [h]
   float* b2s = b1s + h;              // [c]
   float* ls = b2s + c;               // [B] per-sample loss
   int* ys = reinterpret_cast<int*>(ls + B);  // [B]
@@ -216,51 +347,87 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd_kernel(MlpArgs a, float* __r
   auto idx_b2 = [&](int) { return ob2 + (t < c ? t : 0); };
   ParamBatch<8, UPD, TH, AL> pw2;
   ParamBatch<1, UPD, TH, AL> pb1, pb2;
-  if constexpr (PH != 1) {
+  auto load_small = [&] {
     pw2.load(a, wrow, mrow, arow, idx_w2);
     pb1.load(a, wrow, mrow, arow, idx_b1);
     pb2.load(a, wrow, mrow, arow, idx_b2);
+  };
+  if constexpr (PH != 1) {
+    if constexpr (PH != 3) load_small();  // PH 3: after F1 (the registers hold W1 during F1)
     if (t < c) b2s[t] = wrow[ob2 + t];
     if (t < B) ys[t] = static_cast<int>(a.Y[int64_t(agent) * a.ldya + t]);
   }
-  if constexpr (PH == 0)
+  if constexpr (PH == 0 || PH == 3)
     for (int i = t; i < h; i += kThreads) b1s[i] = wrow[ob1 + i];
   if constexpr (PH != 1) __syncthreads();  // PH 1: the staging is the whole LDS (b1 read from memory below)
   float* wsa = ws + int64_t(agent) * B * h;  // H (PH 1 -> 2), then dZ1 for mlp_dw1_kernel
-  if constexpr (PH == 2) {  // H from the F1 kernel
-    for (int o = t; o < B * h; o += kThreads) Hs[(o / h) * hp + (o % h)] = wsa[o];
-  } else {
-
   // ---- F1: Z1^T tiles (32 h x 32 b) on MFMA, K = d in chunks of 32
   const int nht = h / 32, nbt = (B + 31) / 32;
-  const int Bp = 32 * nbt, rows = h + Bp;  // staged rows per chunk (W1 rows, then X rows)
+  const int Bp = 32 * nbt, rows = PH == 3 ? 160 : h + Bp;  // staged rows per chunk (W1 rows, then X rows)
   const int ipw = rows / 32;               // DMA instructions per wave per chunk (8 rows each)
-  const int nk = (d + 31) / 32;
+  const int nk = NK > 0 ? NK : (d + 31) / 32;
   float* stg = lds;
-  auto issue = [&](int kc) {
+  // PH 3 stages through buffer descriptors: one 32-bit lane offset per staged
+  // row serves W1 and momentum alike (chunk kc in the SGPR offset), and the
+  // k >= d pieces of a tail chunk read as zeros (out-of-range lanes): few VGPRs
+  // beside the resident W1, no zeroing pass.
+  const int64_t P1 = int64_t(h) * d + h + int64_t(c) * h + c;
+  const rsrc_t rsW = make_rsrc(wrow, P1 * 4);
+  const rsrc_t rsM = make_rsrc(UPD == 3 && PH == 3 ? mrow : wrow, P1 * 4);
+  const rsrc_t rsX = make_rsrc(xa, (int64_t(B - 1) * a.ldxb + d) * 4);
+  uint32_t voff3[5];  // PH 3: per staged row group i (4 x W1 / momentum, 1 x X)
+  if constexpr (PH == 3) {
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      const int r = 8 * (wave + kWaves * i) + (lane >> 3);
+      const int ch = (lane & 7) ^ (lane >> 3);
+      voff3[i] = i < 4 ? uint32_t((r * d + 4 * ch) * 4) : uint32_t((min(r - h, B - 1) * a.ldxb + 4 * ch) * 4);
+    }
+  }
+  // stage chunk kc of rows [i0 * 32, rows) (W1 / momentum rows from `top`, then X)
+  auto issue = [&](int kc, const float* top, int i0) {
     float* st = stg + (kc % NS) * rows * 32;
-    for (int i = 0; i < ipw; ++i) {
+    if constexpr (PH == 3) {
+      const bool tail = kc == nk - 1 && (d & 31);  // (compile-time false before the last chunk)
+      const bool pok = 32 * kc + 4 * ((lane & 7) ^ (lane >> 3)) < d;
+#pragma unroll
+      for (int i = i0; i < 5; ++i) {
+        const uint32_t vo = !tail || pok ? voff3[i] : kOOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(i < 4 ? (top == wrow ? rsW : rsM) : rsX,
+                                                 DOL_LPTR(st + (wave + kWaves * i) * 256), 16, static_cast<int>(vo),
+                                                 kc * 128, 0, 0);
+      }
+      return;
+    }
+    for (int i = i0; i < ipw; ++i) {
       const int ins = wave + kWaves * i;
       const int r = 8 * ins + (lane >> 3);
       const int ch = (lane & 7) ^ (lane >> 3);
       int k = kc * 32 + 4 * ch;
       k = k < d ? k : 0;  // clamped in-bounds; zeroed after landing
-      const float* src = (r < h) ? wrow + oW1 + int64_t(r) * d + k
+      const float* src = (r < h) ? top + oW1 + int64_t(r) * d + k
                                  : xa + int64_t(min(r - h, B - 1)) * a.ldxb + k;
       __builtin_amdgcn_global_load_lds(DOL_GPTR(src), DOL_LPTR(st + ins * 256), 16, 0, 0);
     }
   };
+  // PH 3: W1[32 wave + li][32 kc + 16 hh + 4 j + q] = wres[kc][j][q] (the last KL chunks: park)
+  f4 wres[PH == 3 ? NK - KL : 1][4];
+  const int i0_b1 = UPD == 3 ? 0 : PH == 3 ? 4 : h / 32;  // PH 3's B1 chunks: momentum rows (UPD 3) + X rows, or X rows only
+  if constexpr (PH == 2) {  // H from the F1 kernel
+    for (int o = t; o < B * h; o += kThreads) Hs[(o / h) * hp + (o % h)] = wsa[o];
+  } else {
+
   f32x16 acc[NT];
 #pragma unroll
   for (int u = 0; u < NT; ++u)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[u][r] = 0.f;
-  for (int s0 = 0; s0 < NS - 1 && s0 < nk; ++s0) issue(s0);
-  for (int kc = 0; kc < nk; ++kc) {
+  for (int s0 = 0; s0 < NS - 1 && s0 < nk; ++s0) issue(s0, wrow, 0);
+  auto f1_chunk = [&](int kc) __attribute__((always_inline)) {
     wait_vmcnt(min(NS - 2, nk - 1 - kc) * ipw);  // chunk kc landed (the next NS - 2 may still fly)
     __builtin_amdgcn_s_barrier();                 // ... for every wave; and stage (kc + NS - 1) % NS is free
     const float* st = stg + (kc % NS) * rows * 32;
-    if (kc == nk - 1 && (d & 31)) {     // zero the clamped k >= d pieces of the tail chunk
+    if (PH != 3 && kc == nk - 1 && (d & 31)) {  // zero the clamped k >= d pieces of the tail chunk
       for (int i = 0; i < ipw; ++i) {
         const int ins = wave + kWaves * i;
         if (kc * 32 + 4 * ((lane & 7) ^ (lane >> 3)) >= d)
@@ -268,7 +435,7 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd_kernel(MlpArgs a, float* __r
       }
       __syncthreads();
     }
-    if (kc + NS - 1 < nk) issue(kc + NS - 1);
+    if (kc + NS - 1 < nk) issue(kc + NS - 1, wrow, 0);
 #pragma unroll
     for (int u = 0; u < NT; ++u) {
       const int tile = wave + kWaves * u;
@@ -281,13 +448,28 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd_kernel(MlpArgs a, float* __r
           const int pos = ((4 * hh + j) ^ (li & 7)) * 4;
           const f4 av = *reinterpret_cast<const f4*>(ar + pos);
           const f4 xv = *reinterpret_cast<const f4*>(xr + pos);
+          if constexpr (PH == 3) {
+            if (kc < NK - KL) wres[kc < NK - KL ? kc : 0][j] = av;
+            else *reinterpret_cast<f4*>(park + ((kc - (NK - KL)) * 16 + wave * 4 + j) * 256 + lane * 4) = av;
+          }
 #pragma unroll
           for (int q = 0; q < 4; ++q) acc[u] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[q], xv[q], acc[u], 0, 0, 0);
         }
       }
     }
+  };
+  if constexpr (PH == 3) {
+#pragma unroll
+    for (int kc = 0; kc < NK; ++kc) f1_chunk(kc);
+  } else {
+    for (int kc = 0; kc < nk; ++kc) f1_chunk(kc);
   }
-  __syncthreads();  // staging is dead: Hs / W2s / Zs reuse it
+  __syncthreads();  // staging is dead: Hs / W2s / Zs reuse it (PH 3: the momentum / X chunks of B1 start landing)
+  // PH 3: B1's first NS - 1 chunks (momentum rows when UPD == 3, then X) fly during F2 .. B2
+  if constexpr (PH == 3) {
+    load_small();
+    for (int s0 = 0; s0 < NS - 1 && s0 < NK; ++s0) issue(s0, mrow, i0_b1);
+  }
   // C/D map: col (b) = lane & 31, row (h) = (r&3) + 8*(r>>2) + 4*(lane>>5)
 #pragma unroll
   for (int u = 0; u < NT; ++u) {
@@ -401,6 +583,13 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd_kernel(MlpArgs a, float* __r
     pb1.commit(a, wrow, grow, mrow, g, idx_b1, ok_b1);
   }
 
+  if constexpr (PH == 3) {
+    DOL_TRACE(3)
+    __syncthreads();  // dZ1 complete in Hs
+    mlp_fused_dw1<UPD, NS, NK, KL>(a, wres, park, Hs, stg, rows, wrow, grow, mrow, issue, i0_b1, ipw);
+    DOL_TRACE(4)
+    return;
+  }
   // dZ1 for the W1 tiles of mlp_dw1_kernel
   for (int o = t; o < B * h; o += kThreads) wsa[o] = Hs[(o / h) * hp + (o % h)];
   DOL_TRACE(3)
@@ -414,18 +603,7 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd_kernel(MlpArgs a, float* __r
 // (loads return 0, stores are dropped), and every load of the tile issued
 // before the MFMA chain (sched_barrier) so the W1 / momentum reads overlap it.
 // KS = MFMA k-steps (2 samples each): 16 for B <= 32, 32 for B <= 64.
-using rsrc_t = __amdgpu_buffer_rsrc_t;
-constexpr uint32_t kOOB = 0x80000000u;  // any lane offset >= every buffer's size
-
-__device__ __forceinline__ rsrc_t make_rsrc(const float* p, int64_t nbytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), 0, static_cast<int>(nbytes), 0x00020000);
-}
-__device__ __forceinline__ float bload(rsrc_t r, uint32_t voff, uint32_t soff) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, static_cast<int>(voff), static_cast<int>(soff), 0));
-}
-__device__ __forceinline__ void bstore_nt(rsrc_t r, uint32_t voff, uint32_t soff, float v) {
-  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, static_cast<int>(voff), static_cast<int>(soff), 2);
-}
+// (buffer helpers: above mlp_fused_dw1)
 
 template <int KS, int UPD, bool TH, bool AL, int CH = 1>
 __global__ __launch_bounds__(kThreads) void mlp_dw1_kernel(MlpArgs a, const float* __restrict__ ws) {
@@ -566,6 +744,18 @@ extern "C" int dol_mlp_step_f32(float* w, int64_t ldw, float* grad, int64_t ldg,
   // alternating pairs on one box (profiles/r03_mlp_dw1_chains.txt) -- the step
   // is not chain-latency bound; DOL_MLP_DW1_CHAINS=1 restores one chain
   static const int dw1_chains = [] { const char* e = getenv("DOL_MLP_DW1_CHAINS"); return e ? atoi(e) : 2; }();
+  // the one-kernel step with W1 resident in registers (mlp_fwd_kernel PH 3;
+  // DOL_MLP_FUSED=1).  It reads W1 once (1.75 instead of 2.16 GB per step at 1024
+  // agents) but its 400 resident floats per lane leave one workgroup per CU:
+  // per agent F1 27-42 us (latency-bound at 4 chunks in flight), F2 + CE 6 and
+  // B2 20 (HBM nearly idle) and B1 66-74 us, 0.588 ms in all vs 0.56 for the two
+  // kernels in the same tool (tools/mlp_phase.hip, profiles/r03_mlp_fused.txt):
+  // kept opt-in.
+  static const int fused = [] { const char* e = getenv("DOL_MLP_FUSED"); return e ? atoi(e) : 0; }();
+  const bool a16 = !(reinterpret_cast<uintptr_t>(mom) & 15) && ldm % 4 == 0 && !(reinterpret_cast<uintptr_t>(grad) & 15) &&
+                   ldg % 4 == 0;
+  const int nkc = (d + 31) / 32;
+  const bool fusable = fused && h == 128 && B <= 32 && a16 && (nkc == 25 || nkc == 4);
   auto go = [&](auto ks, auto upd_c, auto th, auto al) {
     constexpr int KS = decltype(ks)::value, U = decltype(upd_c)::value;
     constexpr bool TH = decltype(th)::value, AL = decltype(al)::value;
@@ -579,6 +769,19 @@ extern "C" int dol_mlp_step_f32(float* w, int64_t ldw, float* grad, int64_t ldg,
       return sizeof(float) * (fwd_union_floats(B, h, c, ns) + h + c + B) + sizeof(int) * size_t(B);
     };
     const bool nt1 = h * ((B + 31) / 32) <= 128;
+    if constexpr (!TH && !AL && U >= 1 && KS == 16) {
+      if (fusable) {
+        auto fz = [&](auto nk_c, auto ns_c) {
+          constexpr int NK = decltype(nk_c)::value, NS = decltype(ns_c)::value;
+          fwd(mlp_fwd_kernel<1, U, false, false, NS, 3, NK>,
+              sizeof(float) * (fwd_union_floats(B, h, c, NS, true, fused_park_chunks(NK, NS)) + h + c + B) +
+                  sizeof(int) * size_t(B));
+        };
+        if (nkc == 25) fz(std::integral_constant<int, 25>{}, std::integral_constant<int, 5>{});
+        else fz(std::integral_constant<int, 4>{}, std::integral_constant<int, 5>{});
+        return;
+      }
+    }
     if (split_fwd) {  // F1 kernel (staging only in LDS), then the per-agent tail kernel
       auto f1 = [&](auto ns_c) {
         constexpr int NS = decltype(ns_c)::value;

@@ -156,3 +156,57 @@ def test_rejects_unsupported_shapes(gpu):
     y = torch.zeros(2, 4, dtype=torch.int64, device=gpu)
     with pytest.raises(ops.DolNativeError, match="multiple of 32"):
         ops.mlp_step(bank.buffer("x"), X, y, 8, 48, 3, grad=bank.buffer("grad"), update=False)
+
+
+_FUSED_CHILD = r"""
+import sys, torch
+sys.path[:0] = sys.argv[1:3]
+from dolhip.bank import AgentBank
+from dolhip.mlp import BatchedMLP, mlp_layout
+out = {}
+for (n, B, d, h, c) in [(8, 32, 784, 128, 10), (3, 7, 100, 128, 5), (2, 32, 128, 128, 10), (5, 20, 800, 128, 3),
+                        (4, 33, 100, 96, 17)]:
+    for mom in (0.0, 0.5):
+        torch.manual_seed(n * 1000 + d)
+        bank = AgentBank(n, mlp_layout(d, h, c), "cuda:0")
+        bank.rows().copy_(torch.randn(n, bank.P) * 0.05)
+        mlp = BatchedMLP(bank, d, h, c)
+        g = torch.Generator().manual_seed(d)
+        for step in range(3):
+            X = torch.randn(n, B, d, generator=g).cuda()
+            y = torch.randint(0, c, (n, B), generator=g).cuda()
+            loss = mlp.step(X, y, lr=0.1, momentum=mom, first_step=(step == 0), write_grad=(step == 2))
+        torch.cuda.synchronize()
+        k = f"{n},{B},{d},{h},{c},{mom}"
+        out[k + ",x"] = bank.rows().cpu().clone()
+        out[k + ",grad"] = bank.rows("grad").cpu().clone()
+        out[k + ",loss"] = loss.cpu().clone()
+        if mom:
+            out[k + ",mom"] = bank.rows("mom").cpu().clone()
+torch.save(out, sys.argv[3])
+print("ok")
+"""
+
+
+def test_fused_one_kernel_step_bit_identical(gpu, tmp_path):
+    """The one-kernel step with W1 resident in registers (DOL_MLP_FUSED=1, read
+    once per process: run in children) gives the same parameters, momentum,
+    gradients and losses as the forward + dW1 kernels, bit for bit: d with and
+    without a partial last chunk, B < 32, plain and momentum SGD, first steps,
+    write_grad, and a shape outside the fused path (falls back)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = {}
+    for v in ("0", "1"):
+        f = str(tmp_path / f"fused{v}.pt")
+        env = dict(os.environ, DOL_MLP_FUSED=v)
+        r = subprocess.run([sys.executable, "-c", _FUSED_CHILD, root,
+                            os.path.join(root, "distributed-optimization-and-learning_amd"), f],
+                           env=env, capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
+        res[v] = torch.load(f, weights_only=True)
+    assert res["0"].keys() == res["1"].keys()
+    for k, t in res["0"].items():
+        assert torch.equal(t, res["1"][k]), k

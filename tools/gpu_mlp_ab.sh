@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/${OUT:-mlp_ab}
 mkdir -p "$OUT"
 for v in ${VARIANTS:-DOL_MLP_DW1_CHAINS=1 DOL_MLP_DW1_CHAINS=2}; do
-  env $(echo $v | tr , " ") timeout -k 10 300 python -u -m pytest tests/test_mlp_gpu.py -x -q --timeout 200 --timeout-method thread > "$OUT/pytest_$v.log" 2>&1
+  env $(echo $v | tr , " ") timeout -k 10 300 python -u -m pytest tests/test_mlp_gpu.py -k "${PYTEST_K:-not bit_identical}" -x -q --timeout 200 --timeout-method thread > "$OUT/pytest_$v.log" 2>&1
   rc=$?; echo "$v pytest rc=$rc $(tail -1 "$OUT/pytest_$v.log")"; [ $rc -eq 0 ] || exit $rc
 done
 for rep in ${REPS:-1 2 3}; do

@@ -61,6 +61,27 @@ int main(int argc, char** argv) {
   const dim3 g2(unsigned((d + 31) / 32 * n));
   hipEvent_t e2;
   CHECK(hipEventCreate(&e2));
+  if (argc > 2 && argv[2][0] == 'f') {  // the one-kernel step (PH 3): phases F1, F2+CE, B2, B1
+    auto k = mlp_fwd_kernel<1, 3, false, false, 5, 3, 25>;
+    const size_t lf = sizeof(float) * (fwd_union_floats(B, h, c, 5, true, fused_park_chunks(25, 5)) + h + c + B) + 4 * B;
+    CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, int(lf)));
+    for (int it = 0; it < 3; ++it) hipLaunchKernelGGL(k, dim3(n), dim3(kThreads), lf, 0, a, ws);
+    CHECK(hipEventRecord(e0));
+    hipLaunchKernelGGL(k, dim3(n), dim3(kThreads), lf, 0, a, ws);
+    CHECK(hipEventRecord(e1));
+    CHECK(hipEventSynchronize(e1));
+    float ms;
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    std::vector<long long> ht(int64_t(n) * 8);
+    CHECK(hipMemcpy(ht.data(), tr, ht.size() * 8, hipMemcpyDeviceToHost));
+    const char* names[] = {"stage+F1", "F2+CE", "B2", "B1+update"};
+    double sum[4] = {0, 0, 0, 0};
+    for (int i = 0; i < n; ++i)
+      for (int p = 0; p < 4; ++p) sum[p] += double(ht[i * 8 + p + 1] - ht[i * 8 + p]);
+    printf("fused kernel %.3f ms (%d agents)\n", ms, n);
+    for (int p = 0; p < 4; ++p) printf("  %-20s %8.1f us\n", names[p], sum[p] / n / 100.0);
+    return 0;
+  }
   for (int it = 0; it < 3; ++it) {
     hipLaunchKernelGGL((mlp_fwd_kernel<1, 3, false, false>), dim3(n), dim3(kThreads), lds, 0, a, ws);
     hipLaunchKernelGGL((mlp_dw1_kernel<16, 3, false, false>), g2, dim3(kThreads), 0, 0, a, ws);
