@@ -344,6 +344,9 @@ __global__ __launch_bounds__(256) void transpose_kernel(const float* __restrict_
   }
 }
 
+// stage order set by dol_pm_set_stage_order (0: DOL_PM_NSEG, else 8)
+int g_pm_nseg = 0;
+
 int env_int(const char* name, int dflt) {
   const char* v = getenv(name);
   return v && *v ? atoi(v) : dflt;
@@ -363,6 +366,19 @@ int n_cus() {
 }  // namespace
 
 extern "C" {
+
+// The best stage order depends on where the bank's pages landed: on one box,
+// process to process, the same mix took 13.35 ms at 8 segments and 12.94 at 32
+// in one process and 11.79 / 12.31 in the next (tools/pm_nseg_sweep.py,
+// profiles/r03_pm_stage_order.txt); dolhip.ops.tune_pm_stage_order picks it per
+// process for the buffers at hand.
+int dol_pm_set_stage_order(int32_t nseg) {
+  if (nseg < 0 || nseg > 256) return fail(DOL_EINVAL, "dol_pm_set_stage_order: segments %d outside [0, 256]", nseg);
+  const int prev = g_pm_nseg;
+  g_pm_nseg = nseg;
+  dol::g_err[0] = '\0';
+  return prev;
+}
 
 }  // extern "C"
 
@@ -438,7 +454,7 @@ int mix_csr_pm_impl(const char* nm, const float* XT, int64_t ldx, int32_t x_rows
     const int lds = NB * SF * 4;
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     const int64_t grid = std::min<int64_t>(ncu, n_stages);
-    int nseg = env_int("DOL_PM_NSEG", 8);
+    int nseg = g_pm_nseg > 0 ? g_pm_nseg : env_int("DOL_PM_NSEG", 8);
     if (nseg < 1 || grid % nseg) nseg = 1;
     hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(grid)), dim3(kT1), lds, s, XT, ldx, x_rows, YT, ldy, n_rows, P,
                        xw, sr, qp_log2, spt, n_stages, nseg, rowptr, col, val, e, nw);

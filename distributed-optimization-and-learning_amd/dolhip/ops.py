@@ -14,7 +14,7 @@ from . import _native
 from ._native import DolNativeError
 
 __all__ = [
-    "DolNativeError", "mix_csr", "mix_ring", "mix_dense", "mix_dense_split3", "dense_split3_workspace_bytes", "split3_x_flags", "er_stochastic",
+    "DolNativeError", "pm_stage_order", "tune_pm_stage_order", "mix_csr", "mix_ring", "mix_dense", "mix_dense_split3", "dense_split3_workspace_bytes", "split3_x_flags", "er_stochastic",
     "mix_ring_steps", "mix_ring_edges", "dgd_ring_edges", "prox_admm_sgd", "admm_dual", "ordered_mean",
     "ordered_sum", "stream_copy", "dual_workspace_bytes", "prox_grad", "admm_step_dual", "mlp_step",
     "dgd_ring", "dgd_csr", "OBJECTIVES", "admm_ls_round", "admm_ls_round_workspace_bytes", "mix_csr_pm",
@@ -110,6 +110,40 @@ def mix_csr_pm(XT: torch.Tensor, YT: torch.Tensor, rowptr: torch.Tensor, col: to
     _native.call("dol_mix_csr_pm_f32", XT.data_ptr(), ldx, x_agents, YT.data_ptr(), ldy, n, P, rowptr.data_ptr(),
                  col.data_ptr() if col.numel() else None, val.data_ptr() if val.numel() else None, _stream(XT))
     return YT
+
+
+def pm_stage_order(nseg: int) -> int:
+    """Set the parameter-major kernels' stage order for this process (nseg
+    regions streamed at once; 0 = the default) and return the previous setting
+    (dol_pm_set_stage_order).  Same bits for every order."""
+    rc = _native.lib().dol_pm_set_stage_order(int(nseg))
+    if rc < 0:
+        raise DolNativeError("dol_pm_set_stage_order: " + _native.lib().dol_last_error().decode(errors="replace"))
+    return rc
+
+
+def tune_pm_stage_order(run, candidates=(8, 16, 32), reps: int = 3) -> dict:
+    """Time `run()` (a parameter-major mix on the buffers it will keep using)
+    under each stage order and keep the fastest for this process: which order
+    balances the HBM channels best depends on where those buffers' pages
+    landed (profiles/r03_pm_stage_order.txt).  Returns {"nseg": best, "ms":
+    {nseg: ms}}.  Setup-time only; results are bit-identical under every order."""
+    dev = torch.cuda.current_device()
+    times = {}
+    for ns in candidates:
+        pm_stage_order(ns)
+        run()
+        torch.cuda.synchronize(dev)
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(reps):
+            run()
+        e.record()
+        torch.cuda.synchronize(dev)
+        times[ns] = s.elapsed_time(e) / reps
+    best = min(times, key=times.get)
+    pm_stage_order(best)
+    return {"nseg": best, "ms": times}
 
 
 SLAB_CHUNK = 64  # DOL_SLAB_CHUNK: agents per LDS chunk of dol_mix_csr_slab_f32

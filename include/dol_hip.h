@@ -74,6 +74,18 @@ int dol_mix_csr_pm_f32(const float* XT, int64_t ldx, int32_t x_rows, float* YT, 
                        int64_t P, const int32_t* rowptr, const int32_t* col, const float* val, hipStream_t s);
 
 /*
+ * Stage order of the parameter-major kernels (dol_mix_csr_pm_f32,
+ * dol_dgd_csr_pm_f32) for this process: the P range is streamed as `nseg`
+ * separate regions at once (a divisor of the CU count; others fall back to 1).
+ * 0 restores the default (DOL_PM_NSEG, else 8).  Results are the same bits for
+ * every order; only the HBM channel balance changes, and with it the speed,
+ * which depends on where the buffers' pages landed.  Returns the previous
+ * setting, or DOL_EINVAL for nseg outside [0, 256].  No reference counterpart
+ * (a launch parameter of this implementation).
+ */
+int dol_pm_set_stage_order(int32_t nseg);
+
+/*
  * dol_mix_csr_f32 for HIGH-DEGREE graphs (tens to thousands of neighbours per
  * row: Erdos-Renyi, dense-ish time-varying W; BASELINE config 5), same
  * reference code (DIST/simulators.py:91-97 + DIST/clients.py:61-69), same

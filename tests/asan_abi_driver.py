@@ -45,6 +45,12 @@ for name, argtypes in _native.SIGNATURES.items():
         calls += 1
         if _native._RESTYPES.get(name) is ctypes.c_int64:
             continue  # workspace-size queries: only must not trip a sanitizer
+        if name == "dol_pm_set_stage_order":  # a setter: 8 / 7 are valid settings, -3 / 2^31-1 are not
+            if (mode in ("neg", "huge")) != (rc == -1):
+                print(f"{name}: {mode} gave rc={rc}")
+                sys.exit(5)
+            L.dol_pm_set_stage_order(0)
+            continue
         if mode in ("null", "neg") and rc != -1:
             print(f"{name} accepted {mode} arguments (rc={rc})")
             sys.exit(3)

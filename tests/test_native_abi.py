@@ -60,6 +60,13 @@ def test_argument_errors_are_reported_without_launch():
     assert rc == -1 and b"workspace" in L.dol_last_error()
 
 
+def test_pm_stage_order_setter():
+    L = _native.lib()
+    assert L.dol_pm_set_stage_order(-1) == -1 and b"outside" in L.dol_last_error()
+    prev = L.dol_pm_set_stage_order(32)
+    assert L.dol_pm_set_stage_order(prev) == 32
+
+
 def test_slab_entry_points_check_arguments():
     L = _native.lib()
     fake = 1 << 20  # never dereferenced

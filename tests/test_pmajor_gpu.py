@@ -87,6 +87,28 @@ def test_pm_mix_stage_orders_bit_identical(nseg, gpu, monkeypatch):
     assert bits_equal(run_pm(X, c, gpu), oracle.mix_csr(X, c.rowptr, c.col, c.val))
 
 
+@pytest.mark.parametrize("nseg", [16, 32, 7])
+def test_pm_stage_order_setter_bit_identical(nseg, gpu):
+    """dol_pm_set_stage_order overrides DOL_PM_NSEG for the process (7 does not
+    divide the grid: one sweep); the tuner keeps the fastest candidate; the bits
+    never change."""
+    torch.manual_seed(2028)
+    c = G.communication_csr("circle", "stochastic", 1000)[0]
+    X = np.random.default_rng(1).standard_normal((1000, 2500)).astype(np.float32)
+    prev = ops.pm_stage_order(nseg)
+    try:
+        assert ops.pm_stage_order(nseg) == nseg
+        assert bits_equal(run_pm(X, c, gpu), oracle.mix_csr(X, c.rowptr, c.col, c.val))
+        XT = torch.as_tensor(np.ascontiguousarray(X.T), device=gpu)
+        YT = torch.empty_like(XT)
+        rp, col, val = csr_dev(c, gpu)
+        tuned = ops.tune_pm_stage_order(lambda: ops.mix_csr_pm(XT, YT, rp, col, val), candidates=(1, 8, 16), reps=1)
+        assert tuned["nseg"] in (1, 8, 16) and ops.pm_stage_order(0) == tuned["nseg"]
+        assert bits_equal(np.ascontiguousarray(YT.cpu().numpy().T), oracle.mix_csr(X, c.rowptr, c.col, c.val))
+    finally:
+        ops.pm_stage_order(prev)
+
+
 def test_pm_mix_long_empty_rectangular_and_nonfinite(gpu):
     rng = np.random.default_rng(5)
     # long rows: the complete graph (degree n - 1) and a dense-ish Erdos-Renyi
