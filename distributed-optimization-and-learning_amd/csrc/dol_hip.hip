@@ -1444,6 +1444,18 @@ int dol_mix_dense_f32(const float* W, int64_t ldw, const float* X, int64_t ldx, 
   return check_launch("dol_mix_dense_f32");
 }
 
+// kernel of dol_mix_ring_steps_f32 chosen by dol_ring_steps_set_variant (0: DOL_RING_STREAM)
+static int g_ring_steps_variant = 0;
+
+int dol_ring_steps_set_variant(int32_t variant) {
+  if (variant < 0 || variant > 2)
+    return fail(DOL_EINVAL, "dol_ring_steps_set_variant: variant %d outside 0 (default) / 1 (tiles) / 2 (stream)", variant);
+  const int prev = g_ring_steps_variant;
+  g_ring_steps_variant = variant;
+  g_err[0] = '\0';
+  return prev;
+}
+
 int dol_mix_ring_steps_f32(const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t n_rows,
                            int64_t P, int32_t steps, const float* w_prev, const float* w_next,
                            hipStream_t s) {
@@ -1466,7 +1478,11 @@ int dol_mix_ring_steps_f32(const float* X, int64_t ldx, float* Y, int64_t ldy, i
   // on another with the same ring round (10.92 ms): no consistent winner, so the
   // r02 default stays.  Clock 1 % below the ring kernel's for both (2424 / 2408
   // vs 2439 MHz, GRBM_GUI_ACTIVE per XCD over the kernel's time).
-  static const int stream = [] { const char* e = getenv("DOL_RING_STREAM"); return e ? atoi(e) : 0; }();
+  // Which of the two wins follows where the bank's pages landed, as for the
+  // parameter-major mix (profiles/r03_pm_stage_order.txt): ops.tune_ring_steps_variant
+  // times both on the buffers in use and keeps the faster (dol_ring_steps_set_variant).
+  static const int stream_env = [] { const char* e = getenv("DOL_RING_STREAM"); return e ? atoi(e) : 0; }();
+  const int stream = g_ring_steps_variant == 0 ? stream_env : g_ring_steps_variant == 2;
   static const int stream_t = [] { const char* e = getenv("DOL_RING_STREAM_T"); return e ? atoi(e) : 1024; }();
   static const int stream_pf = [] { const char* e = getenv("DOL_RING_STREAM_PF"); return e ? atoi(e) : 8; }();
   static const int stream_nt = [] { const char* e = getenv("DOL_RING_STREAM_NT"); return e ? atoi(e) : 1; }();

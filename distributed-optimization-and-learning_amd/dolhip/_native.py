@@ -65,6 +65,7 @@ SIGNATURES = {
     "dol_er_stochastic_f32": [_ptr, _i64, _i32, _f32, ctypes.c_uint64, _ptr],
     "dol_mix_csr_pm_f32": [_ptr, _i64, _i32, _ptr, _i64, _i32, _i64, _ptr, _ptr, _ptr, _ptr],
     "dol_pm_set_stage_order": [_i32],
+    "dol_ring_steps_set_variant": [_i32],
     "dol_dgd_csr_pm_f32": [_ptr, _i64, _i32, _ptr, _i64, _i32, _i64, _ptr, _ptr, _ptr, _ptr, _i64, _ptr, _i64, _i32,
                            _i32, _f32, _f32, ctypes.c_int, _ptr],
     "dol_transpose_f32": [_ptr, _i64, _ptr, _i64, _i64, _i64, _ptr],

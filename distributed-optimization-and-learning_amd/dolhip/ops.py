@@ -14,7 +14,7 @@ from . import _native
 from ._native import DolNativeError
 
 __all__ = [
-    "DolNativeError", "pm_stage_order", "tune_pm_stage_order", "mix_csr", "mix_ring", "mix_dense", "mix_dense_split3", "dense_split3_workspace_bytes", "split3_x_flags", "er_stochastic",
+    "DolNativeError", "pm_stage_order", "tune_pm_stage_order", "ring_steps_variant", "tune_ring_steps_variant", "mix_csr", "mix_ring", "mix_dense", "mix_dense_split3", "dense_split3_workspace_bytes", "split3_x_flags", "er_stochastic",
     "mix_ring_steps", "mix_ring_edges", "dgd_ring_edges", "prox_admm_sgd", "admm_dual", "ordered_mean",
     "ordered_sum", "stream_copy", "dual_workspace_bytes", "prox_grad", "admm_step_dual", "mlp_step",
     "dgd_ring", "dgd_csr", "OBJECTIVES", "admm_ls_round", "admm_ls_round_workspace_bytes", "mix_csr_pm",
@@ -128,10 +128,24 @@ def tune_pm_stage_order(run, candidates=(8, 16, 32), reps: int = 3) -> dict:
     balances the HBM channels best depends on where those buffers' pages
     landed (profiles/r03_pm_stage_order.txt).  Returns {"nseg": best, "ms":
     {nseg: ms}}.  Setup-time only; results are bit-identical under every order."""
+    best, times = _tune(pm_stage_order, run, candidates, reps)
+    return {"nseg": best, "ms": times}
+
+
+def ring_steps_variant(variant: int) -> int:
+    """Kernel of mix_ring_steps for this process: 1 register tiles, 2 streaming,
+    0 default; returns the previous setting (dol_ring_steps_set_variant)."""
+    rc = _native.lib().dol_ring_steps_set_variant(int(variant))
+    if rc < 0:
+        raise DolNativeError("dol_ring_steps_set_variant: " + _native.lib().dol_last_error().decode(errors="replace"))
+    return rc
+
+
+def _tune(setter, run, candidates, reps):
     dev = torch.cuda.current_device()
     times = {}
-    for ns in candidates:
-        pm_stage_order(ns)
+    for c in candidates:
+        setter(c)
         run()
         torch.cuda.synchronize(dev)
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -140,10 +154,19 @@ def tune_pm_stage_order(run, candidates=(8, 16, 32), reps: int = 3) -> dict:
             run()
         e.record()
         torch.cuda.synchronize(dev)
-        times[ns] = s.elapsed_time(e) / reps
+        times[c] = s.elapsed_time(e) / reps
     best = min(times, key=times.get)
-    pm_stage_order(best)
-    return {"nseg": best, "ms": times}
+    setter(best)
+    return best, times
+
+
+def tune_ring_steps_variant(run, reps: int = 3) -> dict:
+    """Time `run()` (a mix_ring_steps call on the buffers it will keep using)
+    with the register-tile and the streaming kernel and keep the faster for
+    this process; which wins depends on where the buffers' pages landed.
+    Returns {"variant": 1 | 2, "ms": {variant: ms}}.  Same bits either way."""
+    best, times = _tune(ring_steps_variant, run, (1, 2), reps)
+    return {"variant": best, "ms": times}
 
 
 SLAB_CHUNK = 64  # DOL_SLAB_CHUNK: agents per LDS chunk of dol_mix_csr_slab_f32

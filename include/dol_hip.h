@@ -86,6 +86,15 @@ int dol_mix_csr_pm_f32(const float* XT, int64_t ldx, int32_t x_rows, float* YT, 
 int dol_pm_set_stage_order(int32_t nseg);
 
 /*
+ * Kernel of dol_mix_ring_steps_f32 for this process: 1 = register tiles
+ * (ring_steps_kernel), 2 = streaming (ring_stream_kernel, used when n_rows >=
+ * 2 * steps + 17), 0 = the default (DOL_RING_STREAM, else tiles).  Same bits
+ * either way.  Returns the previous setting, or DOL_EINVAL outside [0, 2].
+ * No reference counterpart (a launch choice of this implementation).
+ */
+int dol_ring_steps_set_variant(int32_t variant);
+
+/*
  * dol_mix_csr_f32 for HIGH-DEGREE graphs (tens to thousands of neighbours per
  * row: Erdos-Renyi, dense-ish time-varying W; BASELINE config 5), same
  * reference code (DIST/simulators.py:91-97 + DIST/clients.py:61-69), same

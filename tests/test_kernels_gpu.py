@@ -589,13 +589,22 @@ def test_prox_grad_term_vs_oracle(admm, extra, gpu):
     assert bits_equal(gd[:, :P].cpu().numpy(), oracle.prox_grad(g, w, th, al, 0.1))
 
 
+@pytest.fixture(params=[1, 2], ids=["tiles", "stream"])
+def ring_variant(request):
+    """dol_ring_steps_set_variant for the test, restored after it."""
+    prev = ops.ring_steps_variant(request.param)
+    yield request.param
+    ops.ring_steps_variant(prev)
+
+
 @pytest.mark.parametrize("steps", [1, 2, 3, 4, 5, 6, 7, 8])
 @pytest.mark.parametrize("n,P", [(3, 8), (17, 4100), (64, 1024 * 5), (200, 1024), (1001, 2048), (1600, 4100),
                                  (2048, 1024)])
-def test_ring_steps_bit_identical_to_single_rounds(steps, n, P, gpu):
-    """ring_stream_kernel (n >= 2 steps + 9; 512-row tiles: 1600 / 2048 rows have
-    interior tiles, wrap-around edge tiles and a short last tile) and the
-    register-tile kernel (smaller rings)."""
+def test_ring_steps_bit_identical_to_single_rounds(steps, n, P, ring_variant, gpu):
+    """Both kernels of the fused pass: the register tiles and ring_stream_kernel
+    (when n >= 2 steps + 17; 1024-row tiles: 1600 / 2048 rows have interior
+    tiles, wrap-around edge tiles and a short last tile; smaller rings fall back
+    to the tiles)."""
     rng = np.random.default_rng(steps * 100 + n)
     X = rng.standard_normal((n, P)).astype(np.float32)
     wp, wn = rng.random(n).astype(np.float32), rng.random(n).astype(np.float32)
@@ -609,7 +618,7 @@ def test_ring_steps_bit_identical_to_single_rounds(steps, n, P, gpu):
 
 
 @pytest.mark.parametrize("steps", [2, 5, 8])
-def test_ring_steps_interior_tiles(steps, gpu):
+def test_ring_steps_interior_tiles(steps, ring_variant, gpu):
     """ring_stream_kernel's interior path (1024-row tiles with every input row and
     weight in range: here the tiles at rows 1024 and 2048 of 4096) next to the
     wrap-around edge tiles, on a ragged column count."""
@@ -624,6 +633,31 @@ def test_ring_steps_interior_tiles(steps, gpu):
     ops.mix_ring_steps(dev(X, gpu), Y, dev(wp, gpu), dev(wn, gpu), steps)
     torch.cuda.synchronize()
     assert bits_equal(Y.cpu().numpy(), want)
+
+
+def test_ring_steps_variant_tuner(gpu):
+    """tune_ring_steps_variant keeps the faster kernel for the process; the pass
+    gives the same bits after it."""
+    n, P = 1600, 4100
+    rng = np.random.default_rng(7)
+    X = rng.standard_normal((n, P)).astype(np.float32)
+    wp, wn = rng.random(n).astype(np.float32), rng.random(n).astype(np.float32)
+    want = X
+    for _ in range(5):
+        want = oracle.mix_ring(want, wp, wn)
+    Xd, wpd, wnd = dev(X, gpu), dev(wp, gpu), dev(wn, gpu)
+    Y = torch.empty(n, P, device=gpu)
+    prev = ops.ring_steps_variant(0)
+    try:
+        tuned = ops.tune_ring_steps_variant(lambda: ops.mix_ring_steps(Xd, Y, wpd, wnd, 5), reps=1)
+        assert tuned["variant"] in (1, 2) and set(tuned["ms"]) == {1, 2}
+        assert ops.ring_steps_variant(tuned["variant"]) == tuned["variant"]
+        Y.zero_()
+        ops.mix_ring_steps(Xd, Y, wpd, wnd, 5)
+        torch.cuda.synchronize()
+        assert bits_equal(Y.cpu().numpy(), want)
+    finally:
+        ops.ring_steps_variant(prev)
 
 
 @pytest.mark.parametrize("steps", [2, 5, 8])
