@@ -138,9 +138,9 @@ def cpu_baseline(sizes, P: int, seconds: float, full_agents: int):
         torch.manual_seed(2028)
         W = G.communication_graph("circle", "stochastic", n)[0]
         X = torch.randn(n, P)
-        # one warm-up round below 512 agents; the big sample times exactly one round
+        # a warm-up round at every size, then >= 2 timed rounds (>= `seconds` below 512 agents)
         rounds, sec = ref_cpu.time_rounds(W, X, min_seconds=seconds if n < 512 else 0.0,
-                                          max_rounds=50 if n < 512 else 1, warmup=n < 512)
+                                          max_rounds=50 if n < 512 else 2, warmup=True)
         per_n[n] = {"rounds": rounds, "seconds": sec, "rounds_per_s": rounds / sec,
                     "GBps": 2 * n * P * 4 * rounds / sec / 1e9}
         rw = G.csr_from_dense(W).ring_weights()
@@ -180,6 +180,17 @@ def cpu_baseline(sizes, P: int, seconds: float, full_agents: int):
     }
 
 
+def _fit_n2_n(samples: dict, n_full: int):
+    """Least-squares seconds/round = a n^2 + b n over {n: rounds_per_s}, at n_full."""
+    ns = sorted(samples)
+    A = np.array([[n * n, n] for n in ns], dtype=np.float64)
+    t = np.array([1.0 / samples[n] for n in ns])
+    (a, b), *_ = np.linalg.lstsq(A, t, rcond=None)
+    t_full = a * n_full ** 2 + b * n_full
+    return {"rounds_per_s": 1.0 / t_full if t_full > 0 else None, "seconds_per_round": t_full,
+            "a_s_per_agent2": a, "b_s_per_agent": b}
+
+
 def cpu_secondaries(P: int, full_agents: int, admm_sizes=(64, 256), cfg5_sizes=(128, 256), cfg5_agents: int = 1024):
     """CPU legs beside the secondaries (reference-structured torch-CPU code in
     oracle/ref_cpu.py, same threads as cpu_baseline):
@@ -191,35 +202,39 @@ def cpu_secondaries(P: int, full_agents: int, admm_sizes=(64, 256), cfg5_sizes=(
       * config 5: every agent's 784-128-10 MLP step (nn.Module, CrossEntropyLoss,
         SGD momentum, batch 32; DIST/clients.py:34-59) + the consensus round
         with a new ER p = 0.1 W (Neighbors scan + consensus + load_state_dict);
-        Neighbors and consensus grow as n^2, so `value` = the largest n's rate x
-        (n / cfg5_agents)^2 (their share; the linear local steps make it
-        conservative for the GPU's ratio)."""
+        the local steps grow as n and Neighbors + consensus as n^2, so `value`
+        = the least-squares fit seconds/round = a n^2 + b n over the samples,
+        evaluated at cfg5_agents.
+    Every size runs a warm-up round, then 2 timed rounds."""
     from oracle import ref_cpu
     threads = torch.get_num_threads()
     adm = {}
     for n in admm_sizes:
         _log(f"cpu FedADMM: {n} clients x {P}")
-        r, sec = ref_cpu.time_admm_rounds(n, P, warmup=n <= 64)
+        r, sec = ref_cpu.time_admm_rounds(n, P, rounds=2, warmup=True)
         adm[n] = {"rounds": r, "seconds": sec, "rounds_per_s": r / sec, "ms_per_client": sec / r / n * 1e3}
     big = max(admm_sizes)
     c5 = {}
     for n in cfg5_sizes:
         _log(f"cpu config 5: {n} agents")
-        r, sec = ref_cpu.time_config5_rounds(n, warmup=n <= 128)
+        r, sec = ref_cpu.time_config5_rounds(n, rounds=2, warmup=True)
         c5[n] = {"rounds": r, "seconds": sec, "rounds_per_s": r / sec}
     b5 = max(cfg5_sizes)
+    fit5 = _fit_n2_n({n: v["rounds_per_s"] for n, v in c5.items()}, cfg5_agents)
+    if fit5["rounds_per_s"] is None:  # degenerate samples: the per-byte-squared bound instead
+        fit5["rounds_per_s"] = c5[b5]["rounds_per_s"] * (b5 / cfg5_agents) ** 2
     return {
         "fedadmm": {"value": adm[big]["rounds_per_s"] * big / full_agents, "unit": "rounds/s", "cores": threads,
                     "kind": "port", "per_clients": adm,
                     "sample": f"reference-structured torch-CPU FedADMM round (oracle/ref_cpu.py AdmmClient + "
                               f"average_weights), 10 local steps, n in {list(admm_sizes)} x {P}; value = the n={big} "
                               f"rate x {big}/{full_agents} (per client, linear)"},
-        "config5": {"value": c5[b5]["rounds_per_s"] * (b5 / cfg5_agents) ** 2, "unit": "rounds/s", "cores": threads,
-                    "kind": "port", "per_agents": c5,
+        "config5": {"value": fit5["rounds_per_s"], "unit": "rounds/s", "cores": threads,
+                    "kind": "port", "per_agents": c5, "fit_a_n2_plus_b_n": fit5,
                     "sample": f"reference-structured torch-CPU config-5 round (oracle/ref_cpu.py "
                               f"time_config5_rounds: per-agent nn.Module MLP step + ER W Neighbors/consensus), n in "
-                              f"{list(cfg5_sizes)}; value = the n={b5} rate x ({b5}/{cfg5_agents})^2 (the O(n^2) "
-                              f"scan and consensus)"},
+                              f"{list(cfg5_sizes)}, warm-up + 2 rounds each; value = the least-squares fit "
+                              f"seconds/round = a n^2 + b n evaluated at n={cfg5_agents}"},
     }
 
 
@@ -289,10 +304,63 @@ def primal_dual_round(N: int, P: int, world: int, rank: int, device, steps: int,
     return out
 
 
+def _events_ms(fn, reps: int) -> float:
+    """Mean ms of `reps` calls of fn() between two events on the current stream."""
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps
+
+
+RING_STEPS_KERNELS = {1: "ring_steps_kernel (register tiles)", 2: "ring_stream_kernel", 3: "ring_stream_dma_kernel"}
+
+
+def fedlcon_eps_round(device, ring, N: int, P: int, eps: int = 5, reps: int = 10):
+    """Secondary (N = 1): FedLCon's eps consensus rounds as one fused pass over
+    the headline's buffers, through the product call: an AgentBank over
+    ring.x / ring.y and the ring MixingPlan of the same W, bank.mix(plan,
+    steps=eps) exactly as weighted_average/simulators.py:233 calls it.  The
+    first call tunes the kernel for these buffers (ops.mix_ring_steps); every
+    variant's time and the library default's are reported beside the result."""
+    from dolhip import graph as G, ops
+    from dolhip.bank import AgentBank
+    torch.manual_seed(2028)
+    plan = G.MixingPlan(G.communication_csr("circle", "stochastic", N)[0], device)
+    assert plan.kind == "ring"
+    bank = AgentBank(N, P, device, ld=ring.x.stride(0))
+    bank.adopt("x", ring.x)
+    bank.adopt("y", ring.y)
+    bank.mix(plan, steps=eps)  # first use: tunes the eps kernel for this pair of buffers
+    bank.mix(plan, steps=eps)
+    torch.cuda.synchronize(device)
+    ms_pass = _events_ms(lambda: bank.mix(plan, steps=eps), reps)
+    entry = ops.ring_steps_choice(bank.x, bank.y, eps, P=P, n_rows=N)
+    # the untuned library default on the same buffers, for comparison
+    ms_default = _events_ms(lambda: ops.mix_ring_steps(bank.x, bank.y, plan.w_prev, plan.w_next, eps, P=P,
+                                                       n_rows=N, variant=0), reps)
+    ring.x, ring.y = bank.x, bank.y  # (the buffers swapped an even or odd number of times)
+    choice = entry["choice"] if entry else 0
+    return {"eps": eps, "rounds_per_s": eps * 1e3 / ms_pass, "ms_per_pass": ms_pass,
+            "GBps_per_pass": 2 * N * P * 4 / (ms_pass / 1e3) / 1e9,
+            "frac_per_pass": 2 * N * P * 4 / (ms_pass / 1e3) / 1e9 / HBM_PEAK_GBPS,
+            "kernel": RING_STEPS_KERNELS.get(choice, "library default"),
+            "variant_ms": {str(k): v for k, v in (entry["ms"] if entry else {}).items()},
+            "default_ms_per_pass": ms_default, "call": "AgentBank.mix(plan, steps=5) (FedLCon.run's call)",
+            "what": "FedLCon eps=5 consensus rounds fused into one HBM pass, bit-identical; the kernel tuned by the "
+                    "product path for the bank's buffers on first use"}
+
+
 def random_regular_pm_round(device, X, Y, N: int, P: int, reps: int = 10):
     """Secondary (BASELINE config 3's random-regular mix at the headline size):
     X <- W X for a random 4-regular W on the parameter-major bank
-    (dol_mix_csr_pm_f32), reusing the headline's buffers as XT [P, N] / YT."""
+    (dol_mix_csr_pm_f32), reusing the headline's buffers as XT [P, N] / YT.
+    The call is the product one (ops.mix_csr_pm, nseg=None): its first use on
+    these buffers tunes the stage order (the best order follows where the
+    pages landed, profiles/r03_pm_stage_order.txt); the library default's
+    time is reported beside it."""
     from dolhip import graph as G, ops
     c = G.random_regular_csr(N, 4, seed=2028)
     XT = X.view(-1)[: P * N].view(P, N)
@@ -302,22 +370,16 @@ def random_regular_pm_round(device, X, Y, N: int, P: int, reps: int = 10):
     val = torch.as_tensor(c.val, device=device)
     for _ in range(2):
         ops.mix_csr_pm(XT, YT, rp, col, val)
-    # stage order tuned for these buffers (setup, outside the timed region): the
-    # best order follows where the pages landed (profiles/r03_pm_stage_order.txt)
-    tuned = ops.tune_pm_stage_order(lambda: ops.mix_csr_pm(XT, YT, rp, col, val))
     torch.cuda.synchronize(device)
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(reps):
-        ops.mix_csr_pm(XT, YT, rp, col, val)
-    e.record()
-    torch.cuda.synchronize(device)
-    ms = s.elapsed_time(e) / reps
+    ms = _events_ms(lambda: ops.mix_csr_pm(XT, YT, rp, col, val), reps)
+    entry = ops.pm_stage_order_choice(XT, YT, N, P=P)
+    ms_default = _events_ms(lambda: ops.mix_csr_pm(XT, YT, rp, col, val, nseg=0), reps)
     gbps = 2 * N * P * 4 / (ms / 1e3) / 1e9
-    ops.pm_stage_order(0)
     return {"agents": N, "params": P, "degree": 4, "ms_per_round": ms, "rounds_per_s": 1e3 / ms, "GBps": gbps,
             "frac": gbps / HBM_PEAK_GBPS, "kernel": "csr_pm_kernel (parameter-major bank)",
-            "stage_order": tuned["nseg"], "stage_order_ms": {str(k): v for k, v in tuned["ms"].items()},
+            "stage_order": entry["choice"] if entry else 0,
+            "stage_order_ms": {str(k): v for k, v in (entry["ms"] if entry else {}).items()},
+            "default_ms_per_round": ms_default,
             "what": "random 4-regular W mix on the parameter-major bank, bit-identical to the reference consensus"}
 
 
@@ -520,14 +582,13 @@ def main():
     device = torch.device("cuda", int(os.environ.get("DOL_DEVICE_MAP", local)))
     torch.cuda.set_device(device)
     backend = os.environ.get("DOL_DIST_BACKEND", "nccl")
-    if world > 1:
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=device)
-        else:
-            dist.init_process_group(backend)
-
     import dolhip
+    from dolhip import parallel
     from dolhip.parallel import ShardedRing
+    if world > 1:
+        # bounded timeout on every collective + RCCL async error handling: a
+        # stuck rank fails the run instead of hanging it
+        parallel.init_process_group(backend, device=device if backend == "nccl" else None)
 
     dolhip.lib()
     N, P = args.agents, args.params
@@ -573,37 +634,13 @@ def main():
 
     # secondary (N = 1): FedLCon's eps = 5 consensus rounds per local update
     # (DIST/simulators.py:190-196) as ONE temporally blocked pass over the same
-    # X (dol_mix_ring_steps_f32, bit-identical to 5 rounds); the headline above
-    # stays one round per step
+    # X, through the call FedLCon.run makes (weighted_average/simulators.py:233
+    # -> AgentBank.mix(plan, steps=eps) -> MixingPlan.apply_steps ->
+    # ops.mix_ring_steps, whose kernel the product path tunes on first use for
+    # the bank's buffers); the headline above stays one round per step
     fedlcon = None
     if world == 1 and not args.no_primal_dual:
-        from dolhip import ops as _ops
-        eps, reps = 5, 10
-        for _ in range(2):
-            _ops.mix_ring_steps(ring.x, ring.y, ring.w_prev, ring.w_next, eps, P=P, n_rows=N)
-        # kernel (register tiles / streaming) tuned for these buffers, outside the timed region
-        try:
-            tuned_eps = _ops.tune_ring_steps_variant(
-                lambda: _ops.mix_ring_steps(ring.x, ring.y, ring.w_prev, ring.w_next, eps, P=P, n_rows=N))
-        except Exception as exc:  # the secondary keeps the default kernel; the headline line must not fail
-            _log(f"eps kernel tuning failed ({exc}); default kernel")
-            _ops.ring_steps_variant(0)
-            tuned_eps = {"variant": 1, "ms": {}}
-        torch.cuda.synchronize(device)
-        s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s_ev.record()
-        for _ in range(reps):
-            _ops.mix_ring_steps(ring.x, ring.y, ring.w_prev, ring.w_next, eps, P=P, n_rows=N)
-        e_ev.record()
-        torch.cuda.synchronize(device)
-        ms_pass = s_ev.elapsed_time(e_ev) / reps
-        _ops.ring_steps_variant(0)
-        fedlcon = {"eps": eps, "rounds_per_s": eps * 1e3 / ms_pass, "ms_per_pass": ms_pass,
-                   "GBps_per_pass": 2 * N * P * 4 / (ms_pass / 1e3) / 1e9,
-                   "kernel": {1: "ring_steps_kernel (register tiles)", 2: "ring_stream_kernel"}[tuned_eps["variant"]],
-                   "variant_ms": {str(k): v for k, v in tuned_eps["ms"].items()},
-                   "what": "FedLCon eps=5 consensus rounds fused into one HBM pass, bit-identical; the kernel "
-                           "(register tiles / streaming) tuned per process for the buffers in use"}
+        fedlcon = fedlcon_eps_round(device, ring, N, P)
 
     # secondary (N = 1): config 3's random 4-regular mix at the headline size on
     # the parameter-major bank, in the headline's buffers
@@ -631,15 +668,17 @@ def main():
         exact = er_exact_mix_round(device)
     _log("dense ER done")
     cfg5 = None
+    secondary_errors = []
     if not args.no_primal_dual:
         if world == 1:
             cfg5 = config5_round(device)
         else:  # a secondary: an error here must not cost the headline line
             try:
                 cfg5 = config5_round_sharded(device, world, rank)
-            except Exception as e:  # noqa: BLE001
+            except (RuntimeError, ValueError) as e:  # recorded at the line's top level, not hidden
                 cfg5 = {"error": f"{type(e).__name__}: {e}"[:300]}
-                _log(f"config-5 round over ranks failed: {cfg5['error']}")
+                secondary_errors.append({"leg": "config5_round", "error": cfg5["error"]})
+                _log(f"ERROR: config-5 round over ranks failed: {cfg5['error']}")
     _log("config 5 round done")
 
     traffic = None
@@ -653,6 +692,7 @@ def main():
         except (OSError, ValueError):
             traffic = None
 
+    from dolhip import ops
     out = None
     if rank == 0:
         cpu = None
@@ -714,6 +754,8 @@ def main():
             "dense_er_mix": dense,
             "er_exact_mix": exact,
             "config5_round": cfg5,
+            "secondary_errors": secondary_errors,
+            "tuned_launches": ops.tuned_choices(),
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -18,6 +18,7 @@
 #include <string.h>
 #include <stdarg.h>
 #include <algorithm>
+#include <atomic>
 #include <type_traits>
 
 #include "../../include/dol_hip.h"
@@ -54,6 +55,7 @@ using dol::g_err;
 
 constexpr int kThreads = 256;            // 4 waves of 64
 constexpr int64_t kMaxBlocks = int64_t(1) << 24;
+constexpr int kRingStepsVariants = 3;  // highest dol_mix_ring_steps_ex_f32 variant
 
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
@@ -69,6 +71,7 @@ int env_int(const char* name, int dflt) {
 // product and sum rounds once, exactly as the reference's torch CPU ops.
 // ----------------------------------------------------------------------------
 typedef float f4 __attribute__((ext_vector_type(4)));  // native 16-B vector (nontemporal builtins need it)
+typedef uint32_t u4 __attribute__((ext_vector_type(4)));
 
 template <typename V> struct Vec;
 template <> struct Vec<float> {
@@ -489,6 +492,136 @@ __global__ __launch_bounds__(kThreads) void ring_stream_kernel(
     ring_stream_body<S, PF, true, NT>(xc, ldv, Y, ldy, c, n_rows, r0, nT, wprev, wnext);
   else
     ring_stream_body<S, PF, false, NT>(xc, ldv, Y, ldy, c, n_rows, r0, nT, wprev, wnext);
+}
+
+// ----------------------------------------------------------------------------
+// The streaming pass on the headline's load path (r04): the level arithmetic
+// of ring_stream_body (same bits), with the input rows arriving by LDS-DMA
+// (global_load_lds_dwordx4) into a per-wave ring of D 1-KiB rows instead of
+// VGPRs.  Each wave streams its own 1 KiB column strip down the tile and reads
+// back only what it loaded (no barrier; the covering vmcnt orders the wave's
+// own reads), so D - 1 rows per wave stay in flight with no VGPR held for
+// them.  Every step issues exactly one DMA and one store (buffer stores: the
+// 2S prologue steps and the tail store out of range, dropped but counted;
+// past the last input row the DMA re-reads that row into a consumed slot), so
+// one wait, vmcnt(2D - 2), always retires exactly the row about to be read:
+// after L(i) come D - 1 loads and D - 1 stores (the prologue pairs each of its
+// D - 1 loads with a dropped store to keep that count from the first step).
+// Halo rows (the first and last 2S of a tile) load with the default policy,
+// so the neighbouring tile on the same XCD finds them in L2; the rest are
+// nontemporal, as in ring_mix_dma_kernel.
+// ----------------------------------------------------------------------------
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+using rsrc_t = __amdgpu_buffer_rsrc_t;
+constexpr uint32_t kOOB = 0x80000000u;  // a buffer offset past every range: the access is dropped
+
+template <int S, int D, int PF, bool INTERIOR>
+__device__ __forceinline__ void ring_stream_dma_body(const float* __restrict__ X, int64_t ldx, float* __restrict__ Y,
+                                                     int64_t ldy, int64_t c, int n_rows, int r0, int nT,
+                                                     const float* __restrict__ wprev,
+                                                     const float* __restrict__ wnext, float* ring) {
+  static_assert(D == PF || D == 2 * PF, "ring slots are compile-time within a chunk");
+  static_assert(2 * D - 2 <= 63, "vmcnt is 6 bits");
+  const int nsteps = nT + 2 * S;
+  const int ntot = (nsteps + PF - 1) / PF * PF;  // steps run, the tail past nsteps included
+  const int lane = threadIdx.x & 63;
+  auto wrap = [&](int g) {
+    if constexpr (!INTERIOR) g = g < 0 ? g + n_rows : (g >= n_rows ? g - n_rows : g);
+    return g;
+  };
+  int gl = wrap(r0 - S);
+  const float* xc = X + 4 * c;
+  const float* lp = xc + int64_t(gl) * ldx;
+  int issued = 0;
+  auto issue = [&](int j) {  // input index j into slot j % D (j >= nsteps: the last row again)
+    float* dst = ring + (j & (D - 1)) * 256;
+    if (j < 2 * S || j >= nsteps - 2 * S)  // halo rows: default policy (re-read from L2 by the next tile)
+      __builtin_amdgcn_global_load_lds(DOL_GPTR(lp), DOL_LPTR(dst), 16, 0, 0);
+    else
+      __builtin_amdgcn_global_load_lds(DOL_GPTR(lp), DOL_LPTR(dst), 16, 0, 2);
+    if (++issued < nsteps) {
+      ++gl;
+      lp += ldx;
+      if constexpr (!INTERIOR) {
+        if (gl == n_rows) {
+          gl = 0;
+          lp = xc;
+        }
+      }
+    }
+  };
+  const uint32_t voff = static_cast<uint32_t>(c) * 16u;
+  auto store = [&](int i, f4 v) {  // output of step i: row r0 + i - 2S when 2S <= i < nsteps, else dropped
+    const bool ok = i >= 2 * S && i < nsteps;
+    const int r = ok ? r0 + i - 2 * S : r0;
+    const rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(Y + int64_t(r) * ldy, 0, static_cast<int>(ldy * 4), 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), rs, ok ? voff : kOOB, 0, 2);
+  };
+#pragma unroll
+  for (int j = 0; j < D - 1; ++j) {
+    issue(j);
+    store(-1, f4{0.f, 0.f, 0.f, 0.f});
+  }
+  f4 hA[S], hB[S];
+#pragma unroll
+  for (int t = 0; t < S; ++t) hA[t] = hB[t] = f4{0.f, 0.f, 0.f, 0.f};
+  struct Wn { float v[PF + S]; };
+  for (int i0 = 0; i0 < ntot; i0 += PF) {
+    Wn wp, wn;
+    if constexpr (INTERIOR) {
+      wp = *reinterpret_cast<const Wn*>(wprev + (r0 - 2 * S + i0));
+      wn = *reinterpret_cast<const Wn*>(wnext + (r0 - 2 * S + i0));
+    } else {
+#pragma unroll
+      for (int j = 0; j < PF + S; ++j) {
+        const int g = wrap(r0 - 2 * S + min(i0 + j, nsteps + S - 1));
+        wp.v[j] = wprev[g];
+        wn.v[j] = wnext[g];
+      }
+    }
+    const float* slot0 = ring + (D == PF ? 0 : (i0 & (D - 1))) * 256 + lane * 4;
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      const int i = i0 + u;
+      issue(i + D - 1);
+      vm_wait<2 * D - 2>();  // L(i) has landed
+      f4 nv = *reinterpret_cast<const f4*>(slot0 + u * 256);  // level 0 at index i
+#pragma unroll
+      for (int t = 1; t <= S; ++t) {
+        f4& hv = (u & 1) ? hB[t - 1] : hA[t - 1];
+        const f4 old = hv;
+        hv = nv;
+        nv = axpy0(wp.v[u + S - t], old, wn.v[u + S - t], nv);
+      }
+      store(i, nv);
+    }
+  }
+  vm_wait<0>();  // no LDS-DMA may land after the wave's LDS is released
+}
+
+template <int S, int D, int PF>
+__global__ __launch_bounds__(kThreads) void ring_stream_dma_kernel(
+    const float* __restrict__ X, int64_t ldx, float* __restrict__ Y, int64_t ldy, int n_rows,
+    int64_t ncols_v, uint32_t n_col_tiles, const float* __restrict__ wprev,
+    const float* __restrict__ wnext, uint32_t n_row_tiles, int T) {
+  __shared__ __attribute__((aligned(16))) float lds[kThreads / 64][D][256];
+  const uint32_t b = blockIdx.x;
+  const uint32_t x = b & 7u, l = b >> 3;
+  const uint32_t ct = (l / n_row_tiles) * 8 + x;
+  const int r0 = static_cast<int>(l % n_row_tiles) * T;
+  if (ct >= n_col_tiles) return;
+  const int64_t c = int64_t(ct) * kThreads + threadIdx.x;
+  if (c >= ncols_v) return;
+  const int nT = min(T, n_rows - r0);
+  float* ring = &lds[threadIdx.x >> 6][0][0];
+  if (r0 - 2 * S >= 0 && r0 + nT + S + PF <= n_rows)  // every row and weight index in range
+    ring_stream_dma_body<S, D, PF, true>(X, ldx, Y, ldy, c, n_rows, r0, nT, wprev, wnext, ring);
+  else
+    ring_stream_dma_body<S, D, PF, false>(X, ldx, Y, ldy, c, n_rows, r0, nT, wprev, wnext, ring);
 }
 
 // ----------------------------------------------------------------------------
@@ -1444,14 +1577,15 @@ int dol_mix_dense_f32(const float* W, int64_t ldw, const float* X, int64_t ldx, 
   return check_launch("dol_mix_dense_f32");
 }
 
-// kernel of dol_mix_ring_steps_f32 chosen by dol_ring_steps_set_variant (0: DOL_RING_STREAM)
-static int g_ring_steps_variant = 0;
+// kernel of dol_mix_ring_steps_f32 chosen by dol_ring_steps_set_variant (0:
+// DOL_RING_STREAM); atomic, so a setter on one thread never tears a launch's
+// read on another (dol_mix_ring_steps_ex_f32 takes the variant per call)
+static std::atomic<int> g_ring_steps_variant{0};
 
 int dol_ring_steps_set_variant(int32_t variant) {
-  if (variant < 0 || variant > 2)
-    return fail(DOL_EINVAL, "dol_ring_steps_set_variant: variant %d outside 0 (default) / 1 (tiles) / 2 (stream)", variant);
-  const int prev = g_ring_steps_variant;
-  g_ring_steps_variant = variant;
+  if (variant < 0 || variant > kRingStepsVariants)
+    return fail(DOL_EINVAL, "dol_ring_steps_set_variant: variant %d outside 0 (default) / 1 (tiles) / 2 (stream) / 3 (stream, LDS-DMA)", variant);
+  const int prev = g_ring_steps_variant.exchange(variant, std::memory_order_relaxed);
   g_err[0] = '\0';
   return prev;
 }
@@ -1459,7 +1593,15 @@ int dol_ring_steps_set_variant(int32_t variant) {
 int dol_mix_ring_steps_f32(const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t n_rows,
                            int64_t P, int32_t steps, const float* w_prev, const float* w_next,
                            hipStream_t s) {
+  return dol_mix_ring_steps_ex_f32(X, ldx, Y, ldy, n_rows, P, steps, w_prev, w_next, 0, s);
+}
+
+int dol_mix_ring_steps_ex_f32(const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t n_rows,
+                              int64_t P, int32_t steps, const float* w_prev, const float* w_next,
+                              int32_t variant, hipStream_t s) {
   DOL_DIMS_OK("dol_mix_ring_steps_f32", ldx, ldy, P);
+  if (variant < 0 || variant > kRingStepsVariants)
+    return fail(DOL_EINVAL, "dol_mix_ring_steps_ex_f32: variant %d outside 0 (process setting) / 1 (tiles) / 2 (stream) / 3 (stream, LDS-DMA)", variant);
   if (n_rows < 0 || P < 0 || steps < 0) return fail(DOL_EINVAL, "dol_mix_ring_steps_f32: negative size");
   if (n_rows == 0 || P == 0) { g_err[0] = '\0'; return DOL_OK; }
   if (!X || !Y || !w_prev || !w_next) return fail(DOL_EINVAL, "dol_mix_ring_steps_f32: null pointer");
@@ -1482,7 +1624,8 @@ int dol_mix_ring_steps_f32(const float* X, int64_t ldx, float* Y, int64_t ldy, i
   // parameter-major mix (profiles/r03_pm_stage_order.txt): ops.tune_ring_steps_variant
   // times both on the buffers in use and keeps the faster (dol_ring_steps_set_variant).
   static const int stream_env = [] { const char* e = getenv("DOL_RING_STREAM"); return e ? atoi(e) : 0; }();
-  const int stream = g_ring_steps_variant == 0 ? stream_env : g_ring_steps_variant == 2;
+  const int v = variant != 0 ? variant : g_ring_steps_variant.load(std::memory_order_relaxed);
+  const int stream = v == 0 ? stream_env : (v == 2 ? 1 : v == 3 ? 3 : 0);
   static const int stream_t = [] { const char* e = getenv("DOL_RING_STREAM_T"); return e ? atoi(e) : 1024; }();
   static const int stream_pf = [] { const char* e = getenv("DOL_RING_STREAM_PF"); return e ? atoi(e) : 8; }();
   static const int stream_nt = [] { const char* e = getenv("DOL_RING_STREAM_NT"); return e ? atoi(e) : 1; }();
@@ -1506,7 +1649,25 @@ int dol_mix_ring_steps_f32(const float* X, int64_t ldx, float* Y, int64_t ldy, i
     else go_k(ring_stream_kernel<S, PF, false>);
     return check_launch("dol_mix_ring_steps_f32");
   };
+  // variant 3: ring_stream_dma_kernel, D-row LDS-DMA ring per wave (DOL_RING_DMA_D 8 / 16)
+  static const int dma_d = [] { const char* e = getenv("DOL_RING_DMA_D"); return e ? atoi(e) : 8; }();
+  auto go_stream_dma = [&](auto steps_c, int T) {
+    constexpr int S = decltype(steps_c)::value;
+    const int64_t nv = P / 4;
+    const uint32_t nct = static_cast<uint32_t>(cdiv(nv, kThreads));
+    const int64_t nrt = cdiv(n_rows, T);
+    const int64_t grid = cdiv(nct, 8) * 8 * nrt;
+    if (grid > kMaxBlocks) return fail(DOL_EINVAL, "dol_mix_ring_steps_f32: too large");
+    if (dma_d == 16)
+      hipLaunchKernelGGL((ring_stream_dma_kernel<S, 16, 8>), dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, s, X,
+                         ldx, Y, ldy, n_rows, nv, nct, w_prev, w_next, static_cast<uint32_t>(nrt), T);
+    else
+      hipLaunchKernelGGL((ring_stream_dma_kernel<S, 8, 8>), dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, s, X,
+                         ldx, Y, ldy, n_rows, nv, nct, w_prev, w_next, static_cast<uint32_t>(nrt), T);
+    return check_launch("dol_mix_ring_steps_f32");
+  };
   auto go_stream = [&](auto steps_c, int T) {
+    if (stream == 3) return go_stream_dma(steps_c, T);
     if (stream_pf == 16) return go_stream_pf(steps_c, T, std::integral_constant<int, 16>{});
     if (stream_pf == 4) return go_stream_pf(steps_c, T, std::integral_constant<int, 4>{});
     return go_stream_pf(steps_c, T, std::integral_constant<int, 8>{});
@@ -1514,7 +1675,9 @@ int dol_mix_ring_steps_f32(const float* X, int64_t ldx, float* Y, int64_t ldy, i
 
   auto go_v = [&](auto steps_c, auto r_c, auto v_c) {
     constexpr int S = decltype(steps_c)::value, R = decltype(r_c)::value;
-    if (stream && n_rows >= 2 * S + 16 + 1) {  // the stream kernel wraps at most once (PF <= 16)
+    // the stream kernels wrap at most once (PF <= 16); the LDS-DMA one's buffer
+    // stores address a row in 32 bits
+    if (stream && n_rows >= 2 * S + 16 + 1 && (stream != 3 || ldy * 4 < (int64_t(1) << 31))) {
       return go_stream(steps_c, stream_t >= 64 ? stream_t : 1024);
     }
     using V = typename decltype(v_c)::type;

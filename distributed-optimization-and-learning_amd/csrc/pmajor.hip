@@ -32,6 +32,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <atomic>
 #include <type_traits>
 
 #include "../../include/dol_hip.h"
@@ -344,8 +345,9 @@ __global__ __launch_bounds__(256) void transpose_kernel(const float* __restrict_
   }
 }
 
-// stage order set by dol_pm_set_stage_order (0: DOL_PM_NSEG, else 8)
-int g_pm_nseg = 0;
+// stage order set by dol_pm_set_stage_order (0: DOL_PM_NSEG, else 8); atomic,
+// and the _ex entry points take the order per call
+std::atomic<int> g_pm_nseg{0};
 
 int env_int(const char* name, int dflt) {
   const char* v = getenv(name);
@@ -374,8 +376,7 @@ extern "C" {
 // process for the buffers at hand.
 int dol_pm_set_stage_order(int32_t nseg) {
   if (nseg < 0 || nseg > 256) return fail(DOL_EINVAL, "dol_pm_set_stage_order: segments %d outside [0, 256]", nseg);
-  const int prev = g_pm_nseg;
-  g_pm_nseg = nseg;
+  const int prev = g_pm_nseg.exchange(nseg, std::memory_order_relaxed);
   dol::g_err[0] = '\0';
   return prev;
 }
@@ -387,7 +388,8 @@ namespace {
 // obj < 0: the plain mix; else the config-3 round (epilogue e, momentum mode)
 int mix_csr_pm_impl(const char* nm, const float* XT, int64_t ldx, int32_t x_rows, float* YT, int64_t ldy,
                     int32_t n_rows, int64_t P, const int32_t* rowptr, const int32_t* col, const float* val, int obj,
-                    int mode, const PmDgd& e, hipStream_t s) {
+                    int mode, const PmDgd& e, int32_t nseg_req, hipStream_t s) {
+  if (nseg_req < 0 || nseg_req > 256) return fail(DOL_EINVAL, "%s: stage order %d outside [0, 256]", nm, nseg_req);
   if (n_rows < 0 || x_rows < 0 || P < 0) return fail(DOL_EINVAL, "%s: negative size", nm);
   if (n_rows == 0 || P == 0) { dol::g_err[0] = '\0'; return DOL_OK; }
   if (!XT || !YT || !rowptr || (x_rows > 0 && (!col || !val))) return fail(DOL_EINVAL, "%s: null pointer", nm);
@@ -454,7 +456,8 @@ int mix_csr_pm_impl(const char* nm, const float* XT, int64_t ldx, int32_t x_rows
     const int lds = NB * SF * 4;
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     const int64_t grid = std::min<int64_t>(ncu, n_stages);
-    int nseg = g_pm_nseg > 0 ? g_pm_nseg : env_int("DOL_PM_NSEG", 8);
+    const int proc = g_pm_nseg.load(std::memory_order_relaxed);
+    int nseg = nseg_req > 0 ? nseg_req : proc > 0 ? proc : env_int("DOL_PM_NSEG", 8);
     if (nseg < 1 || grid % nseg) nseg = 1;
     hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(grid)), dim3(kT1), lds, s, XT, ldx, x_rows, YT, ldy, n_rows, P,
                        xw, sr, qp_log2, spt, n_stages, nseg, rowptr, col, val, e, nw);
@@ -494,22 +497,36 @@ extern "C" {
 
 int dol_mix_csr_pm_f32(const float* XT, int64_t ldx, int32_t x_rows, float* YT, int64_t ldy, int32_t n_rows,
                        int64_t P, const int32_t* rowptr, const int32_t* col, const float* val, hipStream_t s) {
+  return dol_mix_csr_pm_ex_f32(XT, ldx, x_rows, YT, ldy, n_rows, P, rowptr, col, val, 0, s);
+}
+
+int dol_mix_csr_pm_ex_f32(const float* XT, int64_t ldx, int32_t x_rows, float* YT, int64_t ldy, int32_t n_rows,
+                          int64_t P, const int32_t* rowptr, const int32_t* col, const float* val, int32_t nseg,
+                          hipStream_t s) {
   DOL_DIMS_OK("dol_mix_csr_pm_f32", ldx, ldy, P);
   return mix_csr_pm_impl("dol_mix_csr_pm_f32", XT, ldx, x_rows, YT, ldy, n_rows, P, rowptr, col, val, -1, 0, PmDgd{},
-                         s);
+                         nseg, s);
 }
 
 int dol_dgd_csr_pm_f32(const float* XT, int64_t ldx, int32_t x_rows, float* YT, int64_t ldy, int32_t n_rows,
                        int64_t P, const int32_t* rowptr, const int32_t* col, const float* val, const float* TT,
                        int64_t ldt, float* MT, int64_t ldm, int32_t objective, int32_t local_steps, float lr,
                        float momentum, int first_step, hipStream_t s) {
+  return dol_dgd_csr_pm_ex_f32(XT, ldx, x_rows, YT, ldy, n_rows, P, rowptr, col, val, TT, ldt, MT, ldm, objective,
+                               local_steps, lr, momentum, first_step, 0, s);
+}
+
+int dol_dgd_csr_pm_ex_f32(const float* XT, int64_t ldx, int32_t x_rows, float* YT, int64_t ldy, int32_t n_rows,
+                          int64_t P, const int32_t* rowptr, const int32_t* col, const float* val, const float* TT,
+                          int64_t ldt, float* MT, int64_t ldm, int32_t objective, int32_t local_steps, float lr,
+                          float momentum, int first_step, int32_t nseg, hipStream_t s) {
   DOL_DIMS_OK("dol_dgd_csr_pm_f32", ldx, ldy, P, ldt, ldm);
   const char* nm = "dol_dgd_csr_pm_f32";
   if (objective != 0 && objective != 1) return fail(DOL_EINVAL, "%s: objective must be 0 or 1", nm);
   if (local_steps < 1) return fail(DOL_EINVAL, "%s: local_steps must be >= 1", nm);
   const int mode = momentum == 0.0f ? 0 : (first_step ? 1 : 2);
   const PmDgd e{TT, ldt, mode ? MT : nullptr, mode ? ldm : 0, -lr, momentum, local_steps};
-  return mix_csr_pm_impl(nm, XT, ldx, x_rows, YT, ldy, n_rows, P, rowptr, col, val, objective, mode, e, s);
+  return mix_csr_pm_impl(nm, XT, ldx, x_rows, YT, ldy, n_rows, P, rowptr, col, val, objective, mode, e, nseg, s);
 }
 
 int dol_transpose_f32(const float* A, int64_t lda, float* B, int64_t ldb, int64_t rows, int64_t cols, hipStream_t s) {

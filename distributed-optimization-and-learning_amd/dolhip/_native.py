@@ -33,6 +33,7 @@ SIGNATURES = {
     "dol_last_error": [],
     "dol_mix_csr_f32": [_ptr, _i64, _i32, _ptr, _i64, _i32, _i64, _ptr, _ptr, _ptr, _ptr],
     "dol_mix_ring_steps_f32": [_ptr, _i64, _ptr, _i64, _i32, _i64, _i32, _ptr, _ptr, _ptr],
+    "dol_mix_ring_steps_ex_f32": [_ptr, _i64, _ptr, _i64, _i32, _i64, _i32, _ptr, _ptr, _i32, _ptr],
     "dol_mix_dense_f32": [_ptr, _i64, _ptr, _i64, _ptr, _i64, _i32, _i32, _i64, _ptr],
     "dol_mix_ring_f32": [_ptr, _i64, _ptr, _i64, _i32, _i64, _ptr, _ptr, _ptr, _ptr, _ptr],
     "dol_mix_ring_edges_f32": [_ptr, _i64, _ptr, _i64, _i32, _i64, _ptr, _ptr, _ptr, _ptr, _ptr],
@@ -64,10 +65,13 @@ SIGNATURES = {
     "dol_mix_dense_split3_workspace_bytes": [_i32, _i32, _i64, ctypes.c_int],
     "dol_er_stochastic_f32": [_ptr, _i64, _i32, _f32, ctypes.c_uint64, _ptr],
     "dol_mix_csr_pm_f32": [_ptr, _i64, _i32, _ptr, _i64, _i32, _i64, _ptr, _ptr, _ptr, _ptr],
+    "dol_mix_csr_pm_ex_f32": [_ptr, _i64, _i32, _ptr, _i64, _i32, _i64, _ptr, _ptr, _ptr, _i32, _ptr],
     "dol_pm_set_stage_order": [_i32],
     "dol_ring_steps_set_variant": [_i32],
     "dol_dgd_csr_pm_f32": [_ptr, _i64, _i32, _ptr, _i64, _i32, _i64, _ptr, _ptr, _ptr, _ptr, _i64, _ptr, _i64, _i32,
                            _i32, _f32, _f32, ctypes.c_int, _ptr],
+    "dol_dgd_csr_pm_ex_f32": [_ptr, _i64, _i32, _ptr, _i64, _i32, _i64, _ptr, _ptr, _ptr, _ptr, _i64, _ptr, _i64,
+                              _i32, _i32, _f32, _f32, ctypes.c_int, _i32, _ptr],
     "dol_transpose_f32": [_ptr, _i64, _ptr, _i64, _i64, _i64, _ptr],
     "dol_csr_slab_nk": [_i32],
     "dol_csr_slab_hdr_len": [_i32, _i32],

@@ -93,6 +93,17 @@ class AgentBank:
             self._buf[name] = t
         return t
 
+    def adopt(self, name: str, t: torch.Tensor) -> None:
+        """Use an existing [N, ld] fp32 device matrix as buffer `name` (e.g. a
+        bank over state that was allocated elsewhere)."""
+        if (t.device != self.device or t.dtype != torch.float32 or tuple(t.shape) != (self.n, self.ld)
+                or t.stride(1) != 1 or (self.n > 1 and t.stride(0) != self.ld)):
+            raise ValueError(f"adopt({name!r}): expected a float32 [{self.n}, {self.ld}] row-major matrix on "
+                             f"{self.device}")
+        self._buf[name] = t
+        if name == "x":
+            self.rebind_all()
+
     @property
     def x(self) -> torch.Tensor:
         return self.buffer("x")

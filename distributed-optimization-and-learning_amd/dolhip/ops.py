@@ -6,6 +6,7 @@ stream.  There is deliberately no CPU path: a CPU tensor raises.
 """
 from __future__ import annotations
 
+import os as _os
 from typing import Optional
 
 import torch
@@ -14,7 +15,9 @@ from . import _native
 from ._native import DolNativeError
 
 __all__ = [
-    "DolNativeError", "pm_stage_order", "tune_pm_stage_order", "ring_steps_variant", "tune_ring_steps_variant", "mix_csr", "mix_ring", "mix_dense", "mix_dense_split3", "dense_split3_workspace_bytes", "split3_x_flags", "er_stochastic",
+    "DolNativeError", "pm_stage_order", "tune_pm_stage_order", "ring_steps_variant", "tune_ring_steps_variant",
+    "RING_STEPS_VARIANTS", "PM_STAGE_ORDERS", "tuned_choices", "autotune_enabled", "ring_steps_choice",
+    "pm_stage_order_choice", "mix_csr", "mix_ring", "mix_dense", "mix_dense_split3", "dense_split3_workspace_bytes", "split3_x_flags", "er_stochastic",
     "mix_ring_steps", "mix_ring_edges", "dgd_ring_edges", "prox_admm_sgd", "admm_dual", "ordered_mean",
     "ordered_sum", "stream_copy", "dual_workspace_bytes", "prox_grad", "admm_step_dual", "mlp_step",
     "dgd_ring", "dgd_csr", "OBJECTIVES", "admm_ls_round", "admm_ls_round_workspace_bytes", "mix_csr_pm",
@@ -86,13 +89,14 @@ def mix_csr(X: torch.Tensor, Y: torch.Tensor, rowptr: torch.Tensor, col: torch.T
 
 
 def mix_csr_pm(XT: torch.Tensor, YT: torch.Tensor, rowptr: torch.Tensor, col: torch.Tensor, val: torch.Tensor,
-               x_agents: Optional[int] = None, P: Optional[int] = None) -> torch.Tensor:
+               x_agents: Optional[int] = None, P: Optional[int] = None, nseg: Optional[int] = None) -> torch.Tensor:
     """The gossip mix on the parameter-major bank: YT[p, i] = sum_e val[e] *
     XT[p, col[e]] for every parameter row p (bit-identical to mix_csr on the
     transposed matrices).  XT [P, >= x_agents], YT [P, >= n] (n = rowptr
     length - 1), row strides multiples of 4, 16-B aligned; at most
-    PM_MAX_AGENTS agents.  Reference: DIST/simulators.py:91-97 +
-    DIST/clients.py:61-69."""
+    PM_MAX_AGENTS agents.  nseg: the stage order (None = tuned for these
+    buffers on first use, 0 = the process setting).  Reference:
+    DIST/simulators.py:91-97 + DIST/clients.py:61-69."""
     P = XT.shape[0] if P is None else P
     n = rowptr.shape[0] - 1
     x_agents = n if x_agents is None else int(x_agents)
@@ -107,9 +111,20 @@ def mix_csr_pm(XT: torch.Tensor, YT: torch.Tensor, rowptr: torch.Tensor, col: to
             raise ValueError(f"{nm}: expected contiguous {dt} on {XT.device}")
     if XT.data_ptr() == YT.data_ptr():
         raise ValueError("XT and YT alias: the Jacobi mix needs two buffers")
-    _native.call("dol_mix_csr_pm_f32", XT.data_ptr(), ldx, x_agents, YT.data_ptr(), ldy, n, P, rowptr.data_ptr(),
-                 col.data_ptr() if col.numel() else None, val.data_ptr() if val.numel() else None, _stream(XT))
+
+    def launch(ns):
+        _native.call("dol_mix_csr_pm_ex_f32", XT.data_ptr(), ldx, x_agents, YT.data_ptr(), ldy, n, P,
+                     rowptr.data_ptr(), col.data_ptr() if col.numel() else None,
+                     val.data_ptr() if val.numel() else None, int(ns), _stream(XT))
+    if nseg is None:
+        nseg = _pm_auto(XT, YT, ldx, ldy, x_agents, n, P, launch)
+    launch(nseg)
     return YT
+
+
+def _pm_auto(XT, YT, ldx, ldy, x_agents, n, P, launch) -> int:
+    key = _pair_key("pm", XT, YT, ldx, ldy, x_agents, n, P)
+    return _auto_choice(key, launch, PM_STAGE_ORDERS, (x_agents + n) * P * 4)
 
 
 def pm_stage_order(nseg: int) -> int:
@@ -141,20 +156,28 @@ def ring_steps_variant(variant: int) -> int:
     return rc
 
 
-def _tune(setter, run, candidates, reps):
+def _time_each(run_with, candidates, reps):
+    """{candidate: mean ms of `reps` calls of run_with(candidate)} on the current stream."""
     dev = torch.cuda.current_device()
     times = {}
     for c in candidates:
-        setter(c)
-        run()
+        run_with(c)
         torch.cuda.synchronize(dev)
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
         for _ in range(reps):
-            run()
+            run_with(c)
         e.record()
         torch.cuda.synchronize(dev)
         times[c] = s.elapsed_time(e) / reps
+    return times
+
+
+def _tune(setter, run, candidates, reps):
+    def run_with(c):
+        setter(c)
+        run()
+    times = _time_each(run_with, candidates, reps)
     best = min(times, key=times.get)
     setter(best)
     return best, times
@@ -165,8 +188,73 @@ def tune_ring_steps_variant(run, reps: int = 3) -> dict:
     with the register-tile and the streaming kernel and keep the faster for
     this process; which wins depends on where the buffers' pages landed.
     Returns {"variant": 1 | 2, "ms": {variant: ms}}.  Same bits either way."""
-    best, times = _tune(ring_steps_variant, run, (1, 2), reps)
+    best, times = _tune(ring_steps_variant, run, RING_STEPS_VARIANTS, reps)
     return {"variant": best, "ms": times}
+
+
+# ---------------------------------------------------------------------------
+# Launch choices tuned on the product path.  Which ring-steps kernel / which
+# parameter-major stage order is fastest follows where a bank's pages landed
+# (DESIGN.md §4.1, §4.4), so the first large call on a pair of buffers times
+# every candidate on THOSE buffers (the calls are pure X -> Y mixes: re-running
+# them only rewrites Y) and caches the winner for that (buffer pair, geometry);
+# later calls pass it per call (the _ex entry points), so nothing process-wide
+# changes and the results are the same bits whatever is picked.  A stale entry
+# after the memory is reused can only cost speed.  DOL_AUTOTUNE=0 turns it off
+# (every call then takes the library default).
+# ---------------------------------------------------------------------------
+RING_STEPS_VARIANTS = (1, 2, 3)
+PM_STAGE_ORDERS = (8, 16, 32)
+AUTOTUNE_MIN_BYTES = 1 << 30  # below this one pass is too short to be worth timing
+AUTOTUNE_REPS = 3
+_TUNED: dict = {}
+
+
+def autotune_enabled() -> bool:
+    return _os.environ.get("DOL_AUTOTUNE", "1") != "0"
+
+
+def tuned_choices() -> dict:
+    """{key: {"choice": c, "ms": {candidate: ms}}} of every launch choice this process tuned."""
+    return {repr(k): dict(v) for k, v in _TUNED.items()}
+
+
+def _auto_choice(key, run_with, candidates, nbytes: int) -> int:
+    if not autotune_enabled() or nbytes < AUTOTUNE_MIN_BYTES:
+        return 0
+    hit = _TUNED.get(key)
+    if hit is not None:
+        return hit["choice"]
+    if torch.cuda.is_current_stream_capturing():  # no timing inside a graph capture
+        return 0
+    times = _time_each(run_with, candidates, AUTOTUNE_REPS)
+    best = min(times, key=times.get)
+    _TUNED[key] = {"choice": best, "ms": times}
+    return best
+
+
+def _pair_key(kind, A: torch.Tensor, B: torch.Tensor, *geometry):
+    return (kind, A.device.index, frozenset((A.data_ptr(), B.data_ptr())), *geometry)
+
+
+def _ld(t: torch.Tensor) -> int:
+    return int(t.stride(0) if t.shape[0] > 1 else max(t.shape[1], 1))
+
+
+def ring_steps_choice(X: torch.Tensor, Y: torch.Tensor, steps: int, P: Optional[int] = None,
+                      n_rows: Optional[int] = None) -> Optional[dict]:
+    """The tuned mix_ring_steps entry ({"choice", "ms"}) for this buffer pair, or None."""
+    P = X.shape[1] if P is None else P
+    n = X.shape[0] if n_rows is None else n_rows
+    return _TUNED.get(_pair_key("ring_steps", X, Y, _ld(X), _ld(Y), n, P, int(steps)))
+
+
+def pm_stage_order_choice(XT: torch.Tensor, YT: torch.Tensor, n: int, x_agents: Optional[int] = None,
+                          P: Optional[int] = None) -> Optional[dict]:
+    """The tuned mix_csr_pm / dgd_csr_pm entry ({"choice", "ms"}) for this buffer pair, or None."""
+    P = XT.shape[0] if P is None else P
+    x_agents = n if x_agents is None else int(x_agents)
+    return _TUNED.get(_pair_key("pm", XT, YT, _ld(XT), _ld(YT), x_agents, n, P))
 
 
 SLAB_CHUNK = 64  # DOL_SLAB_CHUNK: agents per LDS chunk of dol_mix_csr_slab_f32
@@ -285,9 +373,12 @@ def transpose(A: torch.Tensor, B: torch.Tensor, rows: Optional[int] = None, cols
 
 
 def mix_ring_steps(X: torch.Tensor, Y: torch.Tensor, w_prev: torch.Tensor, w_next: torch.Tensor, steps: int,
-                   P: Optional[int] = None, n_rows: Optional[int] = None) -> torch.Tensor:
+                   P: Optional[int] = None, n_rows: Optional[int] = None,
+                   variant: Optional[int] = None) -> torch.Tensor:
     """Y = W^steps X for the wrap-around ring in one HBM pass (bit-identical to
-    `steps` mix_ring calls).  Needs P % 4 == 0 and 16-B aligned rows."""
+    `steps` mix_ring calls).  Needs P % 4 == 0 and 16-B aligned rows.
+    variant: the kernel (RING_STEPS_VARIANTS; None = tuned for these buffers
+    on first use, 0 = the process setting)."""
     P = X.shape[1] if P is None else P
     n = X.shape[0] if n_rows is None else n_rows
     ldx = _check_rows("X", X, P)
@@ -297,8 +388,14 @@ def mix_ring_steps(X: torch.Tensor, Y: torch.Tensor, w_prev: torch.Tensor, w_nex
             raise ValueError(f"{nm}: expected contiguous float32 [{n}] on {X.device}")
     if X.data_ptr() == Y.data_ptr():
         raise ValueError("X and Y alias")
-    _native.call("dol_mix_ring_steps_f32", X.data_ptr(), ldx, Y.data_ptr(), ldy, n, P, int(steps),
-                 w_prev.data_ptr(), w_next.data_ptr(), _stream(X))
+
+    def launch(v):
+        _native.call("dol_mix_ring_steps_ex_f32", X.data_ptr(), ldx, Y.data_ptr(), ldy, n, P, int(steps),
+                     w_prev.data_ptr(), w_next.data_ptr(), int(v), _stream(X))
+    if variant is None:
+        variant = _auto_choice(_pair_key("ring_steps", X, Y, ldx, ldy, n, P, int(steps)), launch,
+                               RING_STEPS_VARIANTS, 2 * n * P * 4) if steps > 1 else 0
+    launch(variant)
     return Y
 
 
@@ -382,11 +479,12 @@ def dgd_csr(X: torch.Tensor, Y: torch.Tensor, rowptr: torch.Tensor, col: torch.T
 def dgd_csr_pm(XT: torch.Tensor, YT: torch.Tensor, rowptr: torch.Tensor, col: torch.Tensor, val: torch.Tensor,
                TT: torch.Tensor, MT: Optional[torch.Tensor] = None, objective: str = "least_squares",
                steps: int = 1, lr: float = 0.01, momentum: float = 0.0, first_step: bool = False,
-               x_agents: Optional[int] = None, P: Optional[int] = None) -> torch.Tensor:
+               x_agents: Optional[int] = None, P: Optional[int] = None, nseg: Optional[int] = None) -> torch.Tensor:
     """dgd_csr on the parameter-major bank: XT/YT as mix_csr_pm, TT [P, >= n]
     the targets and MT [P, >= n] the momentum (transposed like XT); the same
     mix and local steps, bit-identical to dgd_csr on the transposed matrices.
-    At most PM_DGD_MAX_AGENTS agents."""
+    At most PM_DGD_MAX_AGENTS agents.  nseg as mix_csr_pm (None: the order
+    tuned for XT / YT, timed on the plain mix, which only writes YT)."""
     P = XT.shape[0] if P is None else P
     n = rowptr.shape[0] - 1
     x_agents = n if x_agents is None else int(x_agents)
@@ -415,10 +513,16 @@ def dgd_csr_pm(XT: torch.Tensor, YT: torch.Tensor, rowptr: torch.Tensor, col: to
         ldm = _check_rows("MT", MT)
         if MT.shape[0] < P or MT.shape[1] < n or MT.device != XT.device:
             raise ValueError(f"MT: expected [>= {P}, >= {n}] on {XT.device}")
-    _native.call("dol_dgd_csr_pm_f32", XT.data_ptr(), ldx, x_agents, YT.data_ptr(), ldy, n, P, rowptr.data_ptr(),
+    if nseg is None:
+        def mix(ns):
+            _native.call("dol_mix_csr_pm_ex_f32", XT.data_ptr(), ldx, x_agents, YT.data_ptr(), ldy, n, P,
+                         rowptr.data_ptr(), col.data_ptr() if col.numel() else None,
+                         val.data_ptr() if val.numel() else None, int(ns), _stream(XT))
+        nseg = _pm_auto(XT, YT, ldx, ldy, x_agents, n, P, mix)
+    _native.call("dol_dgd_csr_pm_ex_f32", XT.data_ptr(), ldx, x_agents, YT.data_ptr(), ldy, n, P, rowptr.data_ptr(),
                  col.data_ptr() if col.numel() else None, val.data_ptr() if val.numel() else None, TT.data_ptr(),
                  ldt, _ptr(MT) if ldm else None, ldm, OBJECTIVES[objective], int(steps), float(lr), float(momentum),
-                 int(bool(first_step)), _stream(XT))
+                 int(bool(first_step)), int(nseg), _stream(XT))
     return YT
 
 

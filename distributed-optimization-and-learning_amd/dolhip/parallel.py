@@ -25,6 +25,8 @@ contiguous blocks, one block per rank:
 """
 from __future__ import annotations
 
+import datetime
+import os
 from typing import List, Optional, Sequence, Tuple
 
 import torch
@@ -32,6 +34,50 @@ import torch.distributed as dist
 
 from . import ops
 from .bank import row_stride
+
+# Fail fast instead of hanging: every collective of the engine's
+# process groups is bounded by this timeout.  The reference has no collectives
+# (its server loop, DEC/servers.py:44-47, and its neighbour reads,
+# DIST/simulators.py:147-152, are in-process), so a stuck peer is a failure
+# mode this engine adds and must surface as an error.
+DEFAULT_TIMEOUT_S = float(os.environ.get("DOL_COLLECTIVE_TIMEOUT_S", "300"))
+
+
+def init_process_group(backend: str, rank: Optional[int] = None, world_size: Optional[int] = None,
+                       device=None, timeout_s: Optional[float] = None) -> None:
+    """torch.distributed.init_process_group with a bounded timeout on every
+    collective and RCCL's asynchronous error handling on: a rank that dies or
+    stops participating makes the others raise (gloo) or abort their
+    communicators (nccl = RCCL: the watchdog tears the process down) within
+    `timeout_s` (DOL_COLLECTIVE_TIMEOUT_S, default 300 s) instead of hanging.
+    The environment switch is set in-process before the group exists (no
+    re-exec).  device: the rank's GPU for nccl (device_id, eager init)."""
+    timeout = datetime.timedelta(seconds=float(DEFAULT_TIMEOUT_S if timeout_s is None else timeout_s))
+    if backend == "nccl":
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+    kw = {"timeout": timeout}
+    if rank is not None:
+        kw["rank"] = rank
+    if world_size is not None:
+        kw["world_size"] = world_size
+    if backend == "nccl" and device is not None:
+        kw["device_id"] = torch.device(device)
+    dist.init_process_group(backend, **kw)
+
+
+def _wait_all(reqs, group=None) -> None:
+    """Wait for point-to-point requests.  gloo: bounded by DEFAULT_TIMEOUT_S on
+    the host (a recv whose peer never sends raises instead of blocking
+    forever).  nccl: a plain wait (the compute stream waits on the transfer,
+    the host does not block; a timeout here would stall the host every round),
+    with the hang bound by the group's timeout + RCCL's async error handling
+    set up by init_process_group."""
+    bounded = dist.get_backend(group) == "gloo"
+    for r in reqs:
+        if bounded:
+            r.wait(datetime.timedelta(seconds=DEFAULT_TIMEOUT_S))
+        else:
+            r.wait()
 
 
 def shard_bounds(n: int, world: int, rank: int) -> Tuple[int, int]:
@@ -108,8 +154,7 @@ class ShardedRing:
         return dist.batch_isend_irecv(ops_)
 
     def _finish_exchange(self, reqs) -> None:
-        for r in reqs:
-            r.wait()
+        _wait_all(reqs, self.group)
         if self._staged():
             self.halo_prev[: self.P].copy_(self._host_halo[0])
             self.halo_next[: self.P].copy_(self._host_halo[1])

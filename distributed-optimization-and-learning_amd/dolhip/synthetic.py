@@ -357,7 +357,7 @@ class TimeVaryingMLPGossip:
         self._side = torch.cuda.Stream(self.device)
         self.X = self.y = None
         self.rounds = 0
-        self.losses = []
+        self.last_loss = None  # the latest round's per-agent losses (round() returns them too)
 
     def batch(self, X: torch.Tensor, y: torch.Tensor) -> None:
         if X.shape[:1] != (self.n_local,) or y.shape[:1] != (self.n_local,) or X.shape[-1] != self.d:
@@ -380,13 +380,18 @@ class TimeVaryingMLPGossip:
             self._plan = G.MixingPlan.from_dense(W, dense_kernel="csr", reuse=self._plan)
         loss = self.mlp.step(self.X, self.y, lr=self.lr, momentum=self.mu, first_step=(self.rounds == 0))
         main.wait_stream(self._side)
+        # the plan's buffers were allocated on the side stream and are read on the
+        # main one: tell the caching allocator, so freeing them never races the mix
+        for t in (self._plan.rowptr, self._plan.col, self._plan.val, self._plan.ent, self._plan.hdr):
+            if t is not None:
+                t.record_stream(main)
         if self.tr is None:
             self.bank.mix(self._plan)
         else:
             self.tr.set_plan(self._plan)
             self.tr.mix(self.bank.rows())
         self.rounds += 1
-        self.losses.append(loss)
+        self.last_loss = loss
         return loss
 
     def params(self) -> torch.Tensor:

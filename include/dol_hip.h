@@ -72,6 +72,11 @@ int dol_mix_csr_f32(const float* X, int64_t ldx, int32_t x_rows,
  */
 int dol_mix_csr_pm_f32(const float* XT, int64_t ldx, int32_t x_rows, float* YT, int64_t ldy, int32_t n_rows,
                        int64_t P, const int32_t* rowptr, const int32_t* col, const float* val, hipStream_t s);
+/* The same call with the stage order given per call (nseg as
+ * dol_pm_set_stage_order; 0 = the process setting).  Same bits for every order. */
+int dol_mix_csr_pm_ex_f32(const float* XT, int64_t ldx, int32_t x_rows, float* YT, int64_t ldy, int32_t n_rows,
+                          int64_t P, const int32_t* rowptr, const int32_t* col, const float* val, int32_t nseg,
+                          hipStream_t s);
 
 /*
  * Stage order of the parameter-major kernels (dol_mix_csr_pm_f32,
@@ -81,7 +86,10 @@ int dol_mix_csr_pm_f32(const float* XT, int64_t ldx, int32_t x_rows, float* YT, 
  * every order; only the HBM channel balance changes, and with it the speed,
  * which depends on where the buffers' pages landed.  Returns the previous
  * setting, or DOL_EINVAL for nseg outside [0, 256].  No reference counterpart
- * (a launch parameter of this implementation).
+ * (a launch parameter of this implementation).  The setting is atomic (a call
+ * on another thread sees the old or the new order, never a torn one); callers
+ * that share the library between threads pass the order per call instead
+ * (dol_mix_csr_pm_ex_f32 / dol_dgd_csr_pm_ex_f32).
  */
 int dol_pm_set_stage_order(int32_t nseg);
 
@@ -90,7 +98,8 @@ int dol_pm_set_stage_order(int32_t nseg);
  * (ring_steps_kernel), 2 = streaming (ring_stream_kernel, used when n_rows >=
  * 2 * steps + 17), 0 = the default (DOL_RING_STREAM, else tiles).  Same bits
  * either way.  Returns the previous setting, or DOL_EINVAL outside [0, 2].
- * No reference counterpart (a launch choice of this implementation).
+ * No reference counterpart (a launch choice of this implementation).  Atomic,
+ * like dol_pm_set_stage_order; dol_mix_ring_steps_ex_f32 takes it per call.
  */
 int dol_ring_steps_set_variant(int32_t variant);
 
@@ -193,6 +202,11 @@ int dol_mix_ring_edges_f32(const float* X, int64_t ldx, float* Y, int64_t ldy, i
 int dol_mix_ring_steps_f32(const float* X, int64_t ldx, float* Y, int64_t ldy,
                            int32_t n_rows, int64_t P, int32_t steps,
                            const float* w_prev, const float* w_next, hipStream_t s);
+/* The same call with the kernel given per call (variant as
+ * dol_ring_steps_set_variant; 0 = the process setting).  Same bits. */
+int dol_mix_ring_steps_ex_f32(const float* X, int64_t ldx, float* Y, int64_t ldy,
+                              int32_t n_rows, int64_t P, int32_t steps,
+                              const float* w_prev, const float* w_next, int32_t variant, hipStream_t s);
 
 /*
  * Dense mix on the matrix cores:  Y[M,P] = W[M,K] . X[K,P]   (fp32 MFMA)
@@ -276,6 +290,11 @@ int dol_dgd_csr_pm_f32(const float* XT, int64_t ldx, int32_t x_rows, float* YT, 
                        int64_t P, const int32_t* rowptr, const int32_t* col, const float* val, const float* TT,
                        int64_t ldt, float* MT, int64_t ldm, int32_t objective, int32_t local_steps, float lr,
                        float momentum, int first_step, hipStream_t s);
+/* dol_dgd_csr_pm_f32 with the stage order per call (see dol_mix_csr_pm_ex_f32). */
+int dol_dgd_csr_pm_ex_f32(const float* XT, int64_t ldx, int32_t x_rows, float* YT, int64_t ldy, int32_t n_rows,
+                          int64_t P, const int32_t* rowptr, const int32_t* col, const float* val, const float* TT,
+                          int64_t ldt, float* MT, int64_t ldm, int32_t objective, int32_t local_steps, float lr,
+                          float momentum, int first_step, int32_t nseg, hipStream_t s);
 
 /*
  * Fused local step of n_agents agents (rows of w/buf/g), replacing:

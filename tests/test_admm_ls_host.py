@@ -19,6 +19,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 import oracle
+from dolhip import parallel
 from conftest import golden
 from oracle import bits_equal
 
@@ -129,7 +130,7 @@ def _free_port():
 def _worker(rank, world, port, N, P, rounds, mean, kw, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    parallel.init_process_group("gloo", rank=rank, world_size=world, timeout_s=120)
     try:
         s = _run(N, P, rounds, mean, **kw)
         q.put((rank, s.lo, s.hi, s.w[:s.n, :P].numpy().copy(), s.alpha[:s.n, :P].numpy().copy(),

@@ -50,14 +50,31 @@ def _csr_dev(c, gpu):
             torch.as_tensor(np.asarray(c.val, np.float32), device=gpu))
 
 
+def _equal_chunked(a, b, what):
+    for p0 in range(0, a.shape[0], 1 << 16):
+        assert torch.equal(a[p0:p0 + (1 << 16)].view(torch.int32), b[p0:p0 + (1 << 16)].view(torch.int32)), \
+            f"{what}: rows {p0}.."
+
+
 def test_pm_mix_8192_full_size(gpu):
+    """Every stage order ops.PM_STAGE_ORDERS offers (what the product path's
+    tuner may pick for these buffers) and the tuned call itself give the same
+    bits; those bits are checked against the oracle and the agent-major kernel."""
     c = G.random_regular_csr(N, 4, seed=2028)  # bench.random_regular_pm_round's W
     rp, col, val = _csr_dev(c, gpu)
     g = torch.Generator(device=gpu).manual_seed(17)
     XT = torch.empty(P, N, device=gpu).normal_(generator=g)  # ld = N = 8192, the bench's view
     YT = torch.empty_like(XT)
-    ops.mix_csr_pm(XT, YT, rp, col, val)
+    ops.mix_csr_pm(XT, YT, rp, col, val, nseg=ops.PM_STAGE_ORDERS[0])
     torch.cuda.synchronize()
+    Yk = torch.empty_like(XT)
+    for nseg in ops.PM_STAGE_ORDERS[1:] + (None,):
+        Yk.fill_(float("nan"))
+        ops.mix_csr_pm(XT, Yk, rp, col, val, nseg=nseg)
+        torch.cuda.synchronize()
+        _equal_chunked(Yk, YT, f"stage order {nseg} vs {ops.PM_STAGE_ORDERS[0]}")
+    del Yk
+    _free()
     # (1) sampled p-rows and whole p-row ranges at the 8 stage segments' starts
     #     and ends (DESIGN §4.1: XCD x walks segment x) vs the oracle
     seg = P // 8
@@ -176,9 +193,13 @@ def test_ring_headline_round_8192_full_size(gpu):
     _free()
 
 
-def test_fedlcon_eps5_pass_8192_full_size(gpu):
+@pytest.mark.parametrize("variant", list(ops.RING_STEPS_VARIANTS))
+def test_fedlcon_eps5_pass_8192_full_size(variant, gpu):
+    """Each kernel the product path's tuner may pick (ops.RING_STEPS_VARIANTS)
+    at the bench's geometry: 2^33 elements, ld = row_stride(2^20)."""
     ring, (wp, wn) = _ring_buffers(gpu)
-    ops.mix_ring_steps(ring.x, ring.y, ring.w_prev, ring.w_next, 5, P=P, n_rows=N)  # bench's call
+    ring.y.fill_(float("nan"))
+    ops.mix_ring_steps(ring.x, ring.y, ring.w_prev, ring.w_next, 5, P=P, n_rows=N, variant=variant)
     torch.cuda.synchronize()
     _check_cols(ring.x, ring.y, wp, wn, 5)
     # sampled rows at every column: each output row depends on 11 input rows
@@ -201,4 +222,30 @@ def test_fedlcon_eps5_pass_8192_full_size(gpu):
             x = y
         assert bits_equal(ring.y[i, :P].cpu().numpy(), x[5]), f"row {i}"
     del ring
+    _free()
+
+
+def test_fedlcon_eps5_product_path_8192_full_size(gpu):
+    """The call FedLCon.run makes (weighted_average/simulators.py:233 ->
+    AgentBank.mix(plan, steps=5) -> MixingPlan.apply_steps -> ops.mix_ring_steps
+    with the kernel tuned for the bank's buffers): the same bits as every
+    variant, and the tuning is recorded for those buffers."""
+    from dolhip.bank import AgentBank
+    ring, (wp, wn) = _ring_buffers(gpu)
+    torch.manual_seed(2028)
+    plan = G.MixingPlan(G.communication_csr("circle", "stochastic", N)[0], gpu)
+    assert plan.kind == "ring"
+    bank = AgentBank(N, P, gpu, ld=ring.x.stride(0))
+    bank.adopt("x", ring.x)
+    bank.adopt("y", ring.y)
+    x0 = ring.x
+    want = torch.empty_like(x0)
+    ops.mix_ring_steps(x0, want, ring.w_prev, ring.w_next, 5, P=P, n_rows=N, variant=ops.RING_STEPS_VARIANTS[0])
+    bank.mix(plan, steps=5)
+    torch.cuda.synchronize()
+    assert bank.x.data_ptr() == ring.y.data_ptr()  # Jacobi swap
+    _equal_chunked(bank.x, want, "bank.mix(plan, 5) vs the tile kernel")
+    keys = [k for k in ops.tuned_choices() if "ring_steps" in k]
+    assert ops.autotune_enabled() and keys, "the product call did not tune the eps kernel"
+    del ring, bank, plan, x0, want
     _free()

@@ -589,7 +589,7 @@ def test_prox_grad_term_vs_oracle(admm, extra, gpu):
     assert bits_equal(gd[:, :P].cpu().numpy(), oracle.prox_grad(g, w, th, al, 0.1))
 
 
-@pytest.fixture(params=[1, 2], ids=["tiles", "stream"])
+@pytest.fixture(params=list(ops.RING_STEPS_VARIANTS), ids=lambda v: {1: "tiles", 2: "stream", 3: "dma"}[v])
 def ring_variant(request):
     """dol_ring_steps_set_variant for the test, restored after it."""
     prev = ops.ring_steps_variant(request.param)
@@ -650,7 +650,7 @@ def test_ring_steps_variant_tuner(gpu):
     prev = ops.ring_steps_variant(0)
     try:
         tuned = ops.tune_ring_steps_variant(lambda: ops.mix_ring_steps(Xd, Y, wpd, wnd, 5), reps=1)
-        assert tuned["variant"] in (1, 2) and set(tuned["ms"]) == {1, 2}
+        assert tuned["variant"] in ops.RING_STEPS_VARIANTS and set(tuned["ms"]) == set(ops.RING_STEPS_VARIANTS)
         assert ops.ring_steps_variant(tuned["variant"]) == tuned["variant"]
         Y.zero_()
         ops.mix_ring_steps(Xd, Y, wpd, wnd, 5)
@@ -658,6 +658,64 @@ def test_ring_steps_variant_tuner(gpu):
         assert bits_equal(Y.cpu().numpy(), want)
     finally:
         ops.ring_steps_variant(prev)
+
+
+def test_ring_steps_autotuned_per_buffers(gpu, monkeypatch):
+    """The product path's tuning (ops.mix_ring_steps with variant=None): the
+    first call on a buffer pair times every variant on those buffers and caches
+    the winner per (pair, geometry) -- the swapped pair hits the same entry --
+    without touching the process-wide setting; the bits never change."""
+    monkeypatch.setattr(ops, "AUTOTUNE_MIN_BYTES", 0)
+    monkeypatch.setattr(ops, "_TUNED", {})
+    n, P = 1600, 4100
+    rng = np.random.default_rng(9)
+    X = rng.standard_normal((n, P)).astype(np.float32)
+    wp, wn = rng.random(n).astype(np.float32), rng.random(n).astype(np.float32)
+    want = X
+    for _ in range(5):
+        want = oracle.mix_ring(want, wp, wn)
+    Xd, wpd, wnd = dev(X, gpu), dev(wp, gpu), dev(wn, gpu)
+    Y = torch.full((n, P), float("nan"), device=gpu)
+    prev = ops.ring_steps_variant(0)
+    ops.mix_ring_steps(Xd, Y, wpd, wnd, 5)
+    torch.cuda.synchronize()
+    assert bits_equal(Y.cpu().numpy(), want)
+    tuned = ops.tuned_choices()
+    assert len(tuned) == 1
+    (entry,) = tuned.values()
+    assert entry["choice"] in ops.RING_STEPS_VARIANTS and set(entry["ms"]) == set(ops.RING_STEPS_VARIANTS)
+    assert ops.ring_steps_variant(0) == 0  # the process setting is untouched
+    ops.mix_ring_steps(Y.clone(), Xd, wpd, wnd, 5)  # a new pair: tuned separately
+    ops.mix_ring_steps(Y, Xd, wpd, wnd, 5)  # the swapped first pair: cached
+    torch.cuda.synchronize()
+    assert len(ops.tuned_choices()) == 2
+    ops.ring_steps_variant(prev)
+
+
+def test_pm_stage_order_autotuned_per_buffers(gpu, monkeypatch):
+    """mix_csr_pm / dgd_csr_pm with nseg=None: the order is tuned once per
+    buffer pair (on the plain mix) and both calls give the bits of an explicit order."""
+    monkeypatch.setattr(ops, "AUTOTUNE_MIN_BYTES", 0)
+    monkeypatch.setattr(ops, "_TUNED", {})
+    from dolhip import graph as G
+    n, P = 1000, 2500
+    c = G.random_regular_csr(n, 4, seed=11)
+    rp, col, val = (torch.as_tensor(a, device=gpu) for a in (c.rowptr, c.col, c.val))
+    rng = np.random.default_rng(4)
+    XT = dev(rng.standard_normal((P, 1000)).astype(np.float32), gpu)
+    TT = dev(rng.standard_normal((P, 1000)).astype(np.float32), gpu)
+    YT = torch.empty_like(XT)
+    want = torch.empty_like(XT)
+    ops.mix_csr_pm(XT, want, rp, col, val, nseg=8)
+    ops.mix_csr_pm(XT, YT, rp, col, val)
+    torch.cuda.synchronize()
+    assert torch.equal(YT.view(torch.int32), want.view(torch.int32))
+    assert len(ops.tuned_choices()) == 1
+    ops.dgd_csr_pm(XT, want, rp, col, val, TT, steps=2, lr=0.1, nseg=16)
+    ops.dgd_csr_pm(XT, YT, rp, col, val, TT, steps=2, lr=0.1)
+    torch.cuda.synchronize()
+    assert torch.equal(YT.view(torch.int32), want.view(torch.int32))
+    assert len(ops.tuned_choices()) == 1  # the dgd round reused the mix's entry
 
 
 @pytest.mark.parametrize("steps", [2, 5, 8])

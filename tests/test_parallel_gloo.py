@@ -64,7 +64,7 @@ def cpu_ordered_sum(W, order, acc_in=None, out=None, scale=1.0, P=None):
 def _worker(rank, world, port, N, P, rounds, order, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    parallel.init_process_group("gloo", rank=rank, world_size=world, timeout_s=120)
     try:
         rng = np.random.default_rng(11)
         X = rng.standard_normal((N, P)).astype(np.float32)
@@ -138,7 +138,7 @@ def _column_worker(rank, world, port, N, P, rounds, q):
     from dolhip import graph as G
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    parallel.init_process_group("gloo", rank=rank, world_size=world, timeout_s=120)
     try:
         csr = G.random_regular_csr(N, 4, seed=5)
         plan = type("Plan", (), {"n_rows": N})()  # host stand-in: the arithmetic is injected
@@ -203,7 +203,7 @@ def cpu_dgd_ring(X, Y, w_prev, w_next, target, mom=None, halo_prev=None, halo_ne
 def _dgd_ring_worker(rank, world, port, N, P, rounds, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    parallel.init_process_group("gloo", rank=rank, world_size=world, timeout_s=120)
     try:
         rng = np.random.default_rng(12)
         X = rng.standard_normal((N, P)).astype(np.float32)
@@ -290,7 +290,7 @@ def test_column_sharded_set_plan_keeps_injected_entries():
 def _transpose_worker(rank, world, port, N, P, rounds, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    parallel.init_process_group("gloo", rank=rank, world_size=world, timeout_s=120)
     try:
         rng = np.random.default_rng(21)
         X = rng.standard_normal((N, P)).astype(np.float32)
@@ -340,3 +340,70 @@ def test_agent_column_transpose_mix_matches_single_process(world, N, P):
         X = ((X * np.float32(0.5)).astype(np.float32) + np.float32(0.25)).astype(np.float32)
         X = oracle.mix_csr(X, c.rowptr, c.col, c.val)
     assert oracle.bits_equal(np.concatenate([r[2] for r in res]), X)
+
+
+def _stall_worker(rank, world, port, what, timeout_s, q):
+    """Rank 0 runs one step of `what`; rank 1 joins the group and then stops
+    participating (alive, silent) for longer than the timeout."""
+    import time
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    parallel.init_process_group("gloo", rank=rank, world_size=world, timeout_s=timeout_s)
+    if rank == 1:
+        time.sleep(3 * timeout_s + 2)
+        q.put((rank, "stalled", 0.0))
+        q.close()
+        q.join_thread()  # flush the queue, then leave without a teardown handshake
+        os._exit(0)
+    saved = parallel.DEFAULT_TIMEOUT_S
+    parallel.DEFAULT_TIMEOUT_S = timeout_s
+    t0 = time.perf_counter()
+    try:
+        N, P = 6, 8
+        if what == "ring":
+            ring = parallel.ShardedRing(N, P, np.ones(N, np.float32), np.ones(N, np.float32), "cpu",
+                                        mix_ring=cpu_mix_ring, mix_edges=cpu_mix_ring_edges)
+            ring.x.zero_()
+            ring.step()
+        elif what == "mean_exact":
+            x = torch.zeros(3, P)
+            parallel.global_mean_exact(x, 0, 3, [4, 0], P, ordered_sum=cpu_ordered_sum)
+        elif what == "mean_fast":
+            x = torch.zeros(3, P)
+            parallel.global_mean(x, [0], 2, P, ordered_sum=cpu_ordered_sum)
+        elif what == "all_to_all":
+            tr = parallel.AgentColumnTranspose(N, P, "cpu", apply=lambda X, Y, P=None: Y)
+            tr.mix(torch.zeros(tr.n_local, P))
+        q.put((rank, "returned", time.perf_counter() - t0))
+    except Exception as e:  # noqa: BLE001 - the point: it raises
+        q.put((rank, type(e).__name__, time.perf_counter() - t0))
+    finally:
+        parallel.DEFAULT_TIMEOUT_S = saved
+        q.close()
+        q.join_thread()
+        os._exit(0)
+
+
+@pytest.mark.parametrize("what", ["ring", "mean_exact", "mean_fast", "all_to_all"])
+def test_stalled_rank_raises_within_timeout(what):
+    """SURVEY §5 fail-fast: when a peer stops participating, the halo exchange,
+    the exact chain mean, the all_reduce mean and config 5's all_to_all raise
+    on the waiting rank within the process group's timeout
+    (parallel.init_process_group) instead of hanging."""
+    timeout_s = 2.0
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_stall_worker, args=(r, 2, port, what, timeout_s, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        res = dict((r, (s, t)) for r, s, t in (q.get(timeout=60) for _ in range(2)))
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    status, elapsed = res[0]
+    assert status != "returned", f"{what}: rank 0 returned although its peer never took part"
+    assert elapsed < 3 * timeout_s, f"{what}: raised only after {elapsed:.1f} s (timeout {timeout_s} s)"

@@ -30,7 +30,7 @@ def _worker(rank, world, port, N, P, rounds, order, q):
     from dolhip import parallel
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    parallel.init_process_group("gloo", rank=rank, world_size=world, timeout_s=120)
     try:
         dev = torch.device("cuda:0")
         rng = np.random.default_rng(5)
@@ -85,7 +85,7 @@ def _column_worker(rank, world, port, N, P, rounds, q):
     from dolhip import graph as G, parallel
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    parallel.init_process_group("gloo", rank=rank, world_size=world, timeout_s=120)
     try:
         dev = torch.device("cuda:0")
         plan = G.MixingPlan(G.random_regular_csr(N, 4, seed=6), dev)
@@ -142,7 +142,7 @@ def _dense_column_worker(rank, world, port, N, P, q):
     from dolhip import graph as G, parallel
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    parallel.init_process_group("gloo", rank=rank, world_size=world, timeout_s=120)
     try:
         dev = torch.device("cuda:0")
         plan = G.MixingPlan.from_dense(G.erdos_renyi_stochastic_hip(N, 0.1, 77, dev))
@@ -190,7 +190,7 @@ def _exact_column_worker(rank, world, port, N, P, q):
     from dolhip import graph as G, parallel
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    parallel.init_process_group("gloo", rank=rank, world_size=world, timeout_s=120)
     try:
         dev = torch.device("cuda:0")
         plan = None
@@ -241,7 +241,7 @@ def _dgd_ring_worker(rank, world, port, N, P, rounds, q):
     from dolhip import parallel
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    parallel.init_process_group("gloo", rank=rank, world_size=world, timeout_s=120)
     try:
         dev = torch.device("cuda:0")
         rng = np.random.default_rng(13)
@@ -294,9 +294,10 @@ def _admm_worker(rank, world, port, N, P, rounds, mean, kw, q):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, os.path.join(root, "distributed-optimization-and-learning_amd"))
     from dolhip.synthetic import SeparableADMM
+    from dolhip import parallel
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    parallel.init_process_group("gloo", rank=rank, world_size=world, timeout_s=120)
     try:
         s = SeparableADMM(N, P, device=torch.device("cuda:0"), mean=mean, **kw)
         for _ in range(rounds):
@@ -357,9 +358,10 @@ def _config5_worker(rank, world, port, N, rounds, q):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, os.path.join(root, "distributed-optimization-and-learning_amd"))
+    from dolhip import parallel
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    parallel.init_process_group("gloo", rank=rank, world_size=world, timeout_s=120)
     try:
         q.put((rank, _config5_sim(N, rounds, torch.device("cuda:0"))))
     finally:
