@@ -337,11 +337,11 @@ def fedlcon_eps_round(device, ring, N: int, P: int, eps: int = 5, reps: int = 10
     bank.mix(plan, steps=eps)
     torch.cuda.synchronize(device)
     ms_pass = _events_ms(lambda: bank.mix(plan, steps=eps), reps)
-    entry = ops.ring_steps_choice(bank.x, bank.y, eps, P=P, n_rows=N)
+    entry = ops.ring_steps_choice(bank.x, bank.buffer("y"), eps, P=P, n_rows=N)
     # the untuned library default on the same buffers, for comparison
-    ms_default = _events_ms(lambda: ops.mix_ring_steps(bank.x, bank.y, plan.w_prev, plan.w_next, eps, P=P,
+    ms_default = _events_ms(lambda: ops.mix_ring_steps(bank.x, bank.buffer("y"), plan.w_prev, plan.w_next, eps, P=P,
                                                        n_rows=N, variant=0), reps)
-    ring.x, ring.y = bank.x, bank.y  # (the buffers swapped an even or odd number of times)
+    ring.x, ring.y = bank.x, bank.buffer("y")  # (the buffers swapped an even or odd number of times)
     choice = entry["choice"] if entry else 0
     return {"eps": eps, "rounds_per_s": eps * 1e3 / ms_pass, "ms_per_pass": ms_pass,
             "GBps_per_pass": 2 * N * P * 4 / (ms_pass / 1e3) / 1e9,

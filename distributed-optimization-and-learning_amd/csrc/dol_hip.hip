@@ -519,7 +519,7 @@ __device__ __forceinline__ void vm_wait() {
 using rsrc_t = __amdgpu_buffer_rsrc_t;
 constexpr uint32_t kOOB = 0x80000000u;  // a buffer offset past every range: the access is dropped
 
-template <int S, int D, int PF, bool INTERIOR>
+template <int S, int D, int PF, bool INTERIOR, int PROBE = 0>
 __device__ __forceinline__ void ring_stream_dma_body(const float* __restrict__ X, int64_t ldx, float* __restrict__ Y,
                                                      int64_t ldy, int64_t c, int n_rows, int r0, int nT,
                                                      const float* __restrict__ wprev,
@@ -557,14 +557,18 @@ __device__ __forceinline__ void ring_stream_dma_body(const float* __restrict__ X
   const uint32_t voff = static_cast<uint32_t>(c) * 16u;
   auto store = [&](int i, f4 v) {  // output of step i: row r0 + i - 2S when 2S <= i < nsteps, else dropped
     const bool ok = i >= 2 * S && i < nsteps;
+    const uint32_t oob = kOOB + (uint32_t(i + D) << 4);  // distinct dropped addresses: no two dummy stores merge
     const int r = ok ? r0 + i - 2 * S : r0;
     const rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(Y + int64_t(r) * ldy, 0, static_cast<int>(ldy * 4), 0x00020000);
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), rs, ok ? voff : kOOB, 0, 2);
+    // nontemporal (2) and volatile (bit 31): the dropped stores must all be
+    // issued -- the vmcnt accounting counts them -- and identical prologue
+    // stores would otherwise be merged by dead-store elimination
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), rs, ok ? voff : oob, 0, int(0x80000002u));
   };
 #pragma unroll
   for (int j = 0; j < D - 1; ++j) {
     issue(j);
-    store(-1, f4{0.f, 0.f, 0.f, 0.f});
+    store(j - D, f4{0.f, 0.f, 0.f, 0.f});
   }
   f4 hA[S], hB[S];
 #pragma unroll
@@ -587,15 +591,20 @@ __device__ __forceinline__ void ring_stream_dma_body(const float* __restrict__ X
 #pragma unroll
     for (int u = 0; u < PF; ++u) {
       const int i = i0 + u;
+      // keep the DMA below the previous step's read and store: the slot it
+      // overwrites was read by that step (WAR), and the store order is counted
+      asm volatile("" ::: "memory");
       issue(i + D - 1);
       vm_wait<2 * D - 2>();  // L(i) has landed
       f4 nv = *reinterpret_cast<const f4*>(slot0 + u * 256);  // level 0 at index i
+      if constexpr (PROBE == 0) {  // PROBE 1 (diagnostics): a copy in this geometry, no levels
 #pragma unroll
-      for (int t = 1; t <= S; ++t) {
-        f4& hv = (u & 1) ? hB[t - 1] : hA[t - 1];
-        const f4 old = hv;
-        hv = nv;
-        nv = axpy0(wp.v[u + S - t], old, wn.v[u + S - t], nv);
+        for (int t = 1; t <= S; ++t) {
+          f4& hv = (u & 1) ? hB[t - 1] : hA[t - 1];
+          const f4 old = hv;
+          hv = nv;
+          nv = axpy0(wp.v[u + S - t], old, wn.v[u + S - t], nv);
+        }
       }
       store(i, nv);
     }
@@ -603,25 +612,33 @@ __device__ __forceinline__ void ring_stream_dma_body(const float* __restrict__ X
   vm_wait<0>();  // no LDS-DMA may land after the wave's LDS is released
 }
 
-template <int S, int D, int PF>
+template <int S, int D, int PF, int PROBE = 0>
 __global__ __launch_bounds__(kThreads) void ring_stream_dma_kernel(
     const float* __restrict__ X, int64_t ldx, float* __restrict__ Y, int64_t ldy, int n_rows,
     int64_t ncols_v, uint32_t n_col_tiles, const float* __restrict__ wprev,
-    const float* __restrict__ wnext, uint32_t n_row_tiles, int T) {
+    const float* __restrict__ wnext, uint32_t n_row_tiles, int T, int order) {
   __shared__ __attribute__((aligned(16))) float lds[kThreads / 64][D][256];
   const uint32_t b = blockIdx.x;
-  const uint32_t x = b & 7u, l = b >> 3;
-  const uint32_t ct = (l / n_row_tiles) * 8 + x;
-  const int r0 = static_cast<int>(l % n_row_tiles) * T;
+  uint32_t ct;
+  int r0;
+  if (order == 0) {  // XCD-aware: an XCD walks its column tiles' row tiles in order (halo rows from L2)
+    const uint32_t x = b & 7u, l = b >> 3;
+    ct = (l / n_row_tiles) * 8 + x;
+    r0 = static_cast<int>(l % n_row_tiles) * T;
+  } else {  // column tile fastest: the chip sweeps row bands, as ring_mix_dma_kernel does
+    const uint32_t nct8 = (n_col_tiles + 7) / 8 * 8;
+    ct = b % nct8;
+    r0 = static_cast<int>(b / nct8) * T;
+  }
   if (ct >= n_col_tiles) return;
   const int64_t c = int64_t(ct) * kThreads + threadIdx.x;
   if (c >= ncols_v) return;
   const int nT = min(T, n_rows - r0);
   float* ring = &lds[threadIdx.x >> 6][0][0];
   if (r0 - 2 * S >= 0 && r0 + nT + S + PF <= n_rows)  // every row and weight index in range
-    ring_stream_dma_body<S, D, PF, true>(X, ldx, Y, ldy, c, n_rows, r0, nT, wprev, wnext, ring);
+    ring_stream_dma_body<S, D, PF, true, PROBE>(X, ldx, Y, ldy, c, n_rows, r0, nT, wprev, wnext, ring);
   else
-    ring_stream_dma_body<S, D, PF, false>(X, ldx, Y, ldy, c, n_rows, r0, nT, wprev, wnext, ring);
+    ring_stream_dma_body<S, D, PF, false, PROBE>(X, ldx, Y, ldy, c, n_rows, r0, nT, wprev, wnext, ring);
 }
 
 // ----------------------------------------------------------------------------
@@ -1651,6 +1668,8 @@ int dol_mix_ring_steps_ex_f32(const float* X, int64_t ldx, float* Y, int64_t ldy
   };
   // variant 3: ring_stream_dma_kernel, D-row LDS-DMA ring per wave (DOL_RING_DMA_D 8 / 16)
   static const int dma_d = [] { const char* e = getenv("DOL_RING_DMA_D"); return e ? atoi(e) : 8; }();
+  // DOL_RING_DMA_ORDER: 0 = XCD-aware row-tile order, 1 = column tile fastest (sweep)
+  static const int dma_order = [] { const char* e = getenv("DOL_RING_DMA_ORDER"); return e ? atoi(e) : 0; }();
   auto go_stream_dma = [&](auto steps_c, int T) {
     constexpr int S = decltype(steps_c)::value;
     const int64_t nv = P / 4;
@@ -1658,12 +1677,21 @@ int dol_mix_ring_steps_ex_f32(const float* X, int64_t ldx, float* Y, int64_t ldy
     const int64_t nrt = cdiv(n_rows, T);
     const int64_t grid = cdiv(nct, 8) * 8 * nrt;
     if (grid > kMaxBlocks) return fail(DOL_EINVAL, "dol_mix_ring_steps_f32: too large");
+    // DOL_RING_DMA_PROBE=1 (diagnostics, wrong results): the same kernel as a copy
+    static const int dma_probe = [] { const char* e = getenv("DOL_RING_DMA_PROBE"); return e ? atoi(e) : 0; }();
+    if constexpr (S == 5) {
+      if (dma_probe == 1) {
+        hipLaunchKernelGGL((ring_stream_dma_kernel<S, 8, 8, 1>), dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, s,
+                           X, ldx, Y, ldy, n_rows, nv, nct, w_prev, w_next, static_cast<uint32_t>(nrt), T, dma_order);
+        return check_launch("dol_mix_ring_steps_f32");
+      }
+    }
     if (dma_d == 16)
       hipLaunchKernelGGL((ring_stream_dma_kernel<S, 16, 8>), dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, s, X,
-                         ldx, Y, ldy, n_rows, nv, nct, w_prev, w_next, static_cast<uint32_t>(nrt), T);
+                         ldx, Y, ldy, n_rows, nv, nct, w_prev, w_next, static_cast<uint32_t>(nrt), T, dma_order);
     else
       hipLaunchKernelGGL((ring_stream_dma_kernel<S, 8, 8>), dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, s, X,
-                         ldx, Y, ldy, n_rows, nv, nct, w_prev, w_next, static_cast<uint32_t>(nrt), T);
+                         ldx, Y, ldy, n_rows, nv, nct, w_prev, w_next, static_cast<uint32_t>(nrt), T, dma_order);
     return check_launch("dol_mix_ring_steps_f32");
   };
   auto go_stream = [&](auto steps_c, int T) {

@@ -605,11 +605,27 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd_kernel(MlpArgs a, float* __r
 // KS = MFMA k-steps (2 samples each): 16 for B <= 32, 32 for B <= 64.
 // (buffer helpers: above mlp_fused_dw1)
 
-template <int KS, int UPD, bool TH, bool AL, int CH = 1>
-__global__ __launch_bounds__(kThreads) void mlp_dw1_kernel(MlpArgs a, const float* __restrict__ ws) {
+// XG (r04): XCD-grouped tile order.  With d = 784 a W1 row is 24.5 lines, so
+// the 128-B column piece of every odd row straddles two lines that the
+// neighbouring tile (dt +- 1) shares; the dispatcher deals consecutive blocks
+// to different XCDs, so with blockIdx = agent * ndt + dt both XCDs fetched
+// (and partially wrote back) those lines.  XG = 1 keeps every tile of an
+// agent on ONE XCD (blockIdx % 8 = agent % 8, tiles in order), so the shared
+// lines meet in that XCD's L2.  Same arithmetic per tile: same bits.
+template <int KS, int UPD, bool TH, bool AL, int CH = 1, int XG = 0>
+__global__ __launch_bounds__(kThreads) void mlp_dw1_kernel(MlpArgs a, const float* __restrict__ ws, int n_agents) {
   const int B = a.B, d = a.d, h = a.h, c = a.c;
   const int ndt = (d + 31) / 32;
-  const int dt = static_cast<int>(blockIdx.x % ndt), agent = static_cast<int>(blockIdx.x / ndt);
+  int dt, agent;
+  if constexpr (XG) {
+    const uint32_t b = blockIdx.x, l = b >> 3;
+    dt = static_cast<int>(l % uint32_t(ndt));
+    agent = static_cast<int>((l / uint32_t(ndt)) * 8 + (b & 7));
+    if (agent >= n_agents) return;
+  } else {
+    dt = static_cast<int>(blockIdx.x % ndt);
+    agent = static_cast<int>(blockIdx.x / ndt);
+  }
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int li = lane & 31, hh = lane >> 5;
@@ -736,7 +752,9 @@ extern "C" int dol_mlp_step_f32(float* w, int64_t ldw, float* grad, int64_t ldg,
   static const int split_fwd = [] { const char* e = getenv("DOL_MLP_SPLIT_FWD"); return e ? atoi(e) : 0; }();
   const int upd = update ? mode + 1 : 0;
   float* ws = static_cast<float*>(work);
-  const int64_t n_blk2 = int64_t((d + 31) / 32) * n_agents;
+  // dW1 tile order (DOL_MLP_DW1_XCD: 1 = an agent's tiles on one XCD, 0 = agent-major)
+  static const int dw1_xcd = [] { const char* e = getenv("DOL_MLP_DW1_XCD"); return e ? atoi(e) : 1; }();
+  const int64_t n_blk2 = int64_t((d + 31) / 32) * (dw1_xcd ? (int64_t(n_agents) + 7) / 8 * 8 : n_agents);
   if (n_blk2 > (int64_t(1) << 31) - 1) return fail(DOL_EINVAL, "dol_mlp_step_f32: too many W1 tiles for one launch");
   const dim3 grid2(static_cast<unsigned>(n_blk2));
   // dW1's k-chain as two interleaved accumulators summed at the end (VERDICT r02
@@ -805,10 +823,12 @@ extern "C" int dol_mlp_step_f32(float* w, int64_t ldw, float* grad, int64_t ldg,
       if (nt1) fwd(mlp_fwd_kernel<1, U, TH, AL>, lds);
       else fwd(mlp_fwd_kernel<4, U, TH, AL>, lds);
     }
-    if (dw1_chains == 2)
-      hipLaunchKernelGGL((mlp_dw1_kernel<KS, U, TH, AL, 2>), grid2, block, 0, s, a, ws);
+    if (dw1_xcd)
+      hipLaunchKernelGGL((mlp_dw1_kernel<KS, U, TH, AL, 2, 1>), grid2, block, 0, s, a, ws, n_agents);
+    else if (dw1_chains == 2)
+      hipLaunchKernelGGL((mlp_dw1_kernel<KS, U, TH, AL, 2>), grid2, block, 0, s, a, ws, n_agents);
     else
-      hipLaunchKernelGGL((mlp_dw1_kernel<KS, U, TH, AL>), grid2, block, 0, s, a, ws);
+      hipLaunchKernelGGL((mlp_dw1_kernel<KS, U, TH, AL>), grid2, block, 0, s, a, ws, n_agents);
   };
   auto by_upd = [&](auto ks, auto th, auto al) {
     using std::integral_constant;

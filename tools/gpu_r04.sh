@@ -15,9 +15,12 @@ if [ -n "$TESTS" ]; then
   if crash $rc; then exit $rc; fi
 fi
 if [ -n "$EPS" ]; then
-  for d in 8 16; do
-    DOL_RING_DMA_D=$d timeout -k 10 300 python -u tools/eps_variants.py $EPS_ARGS >> "$OUT/eps.jsonl" 2> "$OUT/eps.err"
-    rc=$?; echo "eps D=$d rc=$rc"; tail -1 "$OUT/eps.jsonl"
+  # EPS_ENVS: space-separated env assignments, one run each (comma-joined for several vars)
+  for e in ${EPS_ENVS:-DOL_RING_DMA_D=8 DOL_RING_DMA_D=16}; do
+    env ${e//,/ } timeout -k 10 300 python -u tools/eps_variants.py $EPS_ARGS > "$OUT/eps_one.json" 2>> "$OUT/eps.err"
+    rc=$?; echo "eps $e rc=$rc"
+    python -c "import json,sys; d=json.load(open('$OUT/eps_one.json')); d['env']='$e'; print(json.dumps(d))" >> "$OUT/eps.jsonl"
+    tail -1 "$OUT/eps.jsonl" | cut -c1-400
     if crash $rc; then exit $rc; fi
   done
 fi

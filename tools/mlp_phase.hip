@@ -84,12 +84,12 @@ int main(int argc, char** argv) {
   }
   for (int it = 0; it < 3; ++it) {
     hipLaunchKernelGGL((mlp_fwd_kernel<1, 3, false, false>), dim3(n), dim3(kThreads), lds, 0, a, ws);
-    hipLaunchKernelGGL((mlp_dw1_kernel<16, 3, false, false>), g2, dim3(kThreads), 0, 0, a, ws);
+    hipLaunchKernelGGL((mlp_dw1_kernel<16, 3, false, false>), g2, dim3(kThreads), 0, 0, a, ws, n);
   }
   CHECK(hipEventRecord(e0));
   hipLaunchKernelGGL((mlp_fwd_kernel<1, 3, false, false>), dim3(n), dim3(kThreads), lds, 0, a, ws);
   CHECK(hipEventRecord(e2));
-  hipLaunchKernelGGL((mlp_dw1_kernel<16, 3, false, false>), g2, dim3(kThreads), 0, 0, a, ws);
+  hipLaunchKernelGGL((mlp_dw1_kernel<16, 3, false, false>), g2, dim3(kThreads), 0, 0, a, ws, n);
   CHECK(hipEventRecord(e1));
   CHECK(hipEventSynchronize(e1));
   float ms, ms_fwd;
