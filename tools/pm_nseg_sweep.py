@@ -38,18 +38,18 @@ def main():
     wp, wn = torch.rand(N, device=dev), torch.rand(N, device=dev)
     c = G.random_regular_csr(N, 4, seed=2028)
     rp, col, val = (torch.as_tensor(t, device=dev) for t in (c.rowptr, c.col, c.val))
-    pm = lambda: ops.mix_csr_pm(X.view(P, N), Y.view(P, N), rp, col, val)  # noqa: E731
+    def pm(ns):
+        return lambda: ops.mix_csr_pm(X.view(P, N), Y.view(P, N), rp, col, val, nseg=ns)
     res = {"ring_ms": timed(lambda: ops.mix_ring(X, Y, wp, wn))}
-    for ns in (1, 2, 4, 8, 16, 32, 64):
-        os.environ["DOL_PM_NSEG"] = str(ns)
-        res[f"pm_nseg{ns}_ms"] = timed(pm)
+    for ns in (1, 2, 4, 8, 16, 32, 64, 128, 256):
+        res[f"pm_nseg{ns}_ms"] = timed(pm(ns))
     os.environ["DOL_PM_VARIANT"] = "4"
-    for ns in (8, 16, 32):
-        os.environ["DOL_PM_NSEG"] = str(ns)
-        res[f"pm_geometry_copy_nseg{ns}_ms"] = timed(pm)
+    for ns in (8, 16, 32, 64, 256):
+        res[f"pm_geometry_copy_nseg{ns}_ms"] = timed(pm(ns))
     os.environ.pop("DOL_PM_VARIANT")
-    os.environ.pop("DOL_PM_NSEG")
-    res["pm_default_ms"] = timed(pm)
+    res["pm_default_ms"] = timed(pm(0))
+    res["pm_tuned_ms"] = timed(pm(None))
+    res["pm_tuned"] = ops.pm_stage_order_choice(Y.view(P, N), X.view(P, N), N, P=P)
     res["ring_ms_again"] = timed(lambda: ops.mix_ring(X, Y, wp, wn))
     print(json.dumps(res), flush=True)
 
