@@ -1457,6 +1457,62 @@ int dol_version(void) { return 100; }
 
 const char* dol_last_error(void) { return g_err; }
 
+// A bank buffer as ONE physical allocation (hipMemCreate) mapped into a
+// reserved VA range, instead of whatever hipMalloc's suballocator returns
+// (tools/alloc_probe.hip measures the ring round on both).
+int dol_bank_alloc(int64_t bytes, void** ptr, int64_t* mapped_bytes) {
+  if (!ptr || !mapped_bytes || bytes <= 0 || bytes > 4 * dol::kMaxDim)
+    return fail(DOL_EINVAL, "dol_bank_alloc: bad arguments");
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return fail(DOL_EINVAL, "dol_bank_alloc: no device");
+  *ptr = nullptr;
+  *mapped_bytes = 0;
+  hipMemAllocationProp prop{};
+  prop.type = hipMemAllocationTypePinned;
+  prop.location.type = hipMemLocationTypeDevice;
+  prop.location.id = dev;
+  size_t gran = 0;
+  hipError_t e = hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended);
+  if (e != hipSuccess || gran == 0) return fail(-static_cast<int>(e ? e : hipErrorInvalidValue), "dol_bank_alloc: granularity: %s", hipGetErrorString(e));
+  const size_t size = (static_cast<size_t>(bytes) + gran - 1) / gran * gran;
+  hipMemGenericAllocationHandle_t h{};
+  if ((e = hipMemCreate(&h, size, &prop, 0)) != hipSuccess)
+    return fail(-static_cast<int>(e), "dol_bank_alloc: hipMemCreate(%zu): %s", size, hipGetErrorString(e));
+  void* va = nullptr;
+  if ((e = hipMemAddressReserve(&va, size, gran, nullptr, 0)) != hipSuccess) {
+    (void)hipMemRelease(h);
+    return fail(-static_cast<int>(e), "dol_bank_alloc: hipMemAddressReserve: %s", hipGetErrorString(e));
+  }
+  if ((e = hipMemMap(va, size, 0, h, 0)) != hipSuccess) {
+    (void)hipMemAddressFree(va, size);
+    (void)hipMemRelease(h);
+    return fail(-static_cast<int>(e), "dol_bank_alloc: hipMemMap: %s", hipGetErrorString(e));
+  }
+  (void)hipMemRelease(h);  // the mapping keeps the memory until it is unmapped
+  hipMemAccessDesc acc{};
+  acc.location = prop.location;
+  acc.flags = hipMemAccessFlagsProtReadWrite;
+  if ((e = hipMemSetAccess(va, size, &acc, 1)) != hipSuccess) {
+    (void)hipMemUnmap(va, size);
+    (void)hipMemAddressFree(va, size);
+    return fail(-static_cast<int>(e), "dol_bank_alloc: hipMemSetAccess: %s", hipGetErrorString(e));
+  }
+  *ptr = va;
+  *mapped_bytes = static_cast<int64_t>(size);
+  g_err[0] = '\0';
+  return DOL_OK;
+}
+
+int dol_bank_free(void* ptr, int64_t mapped_bytes) {
+  if (!ptr) return DOL_OK;
+  if (mapped_bytes <= 0 || mapped_bytes > 8 * dol::kMaxDim) return fail(DOL_EINVAL, "dol_bank_free: bad size");
+  hipError_t e = hipMemUnmap(ptr, static_cast<size_t>(mapped_bytes));
+  if (e == hipSuccess) e = hipMemAddressFree(ptr, static_cast<size_t>(mapped_bytes));
+  if (e != hipSuccess) return fail(-static_cast<int>(e), "dol_bank_free: %s", hipGetErrorString(e));
+  g_err[0] = '\0';
+  return DOL_OK;
+}
+
 int dol_mix_csr_f32(const float* X, int64_t ldx, int32_t x_rows, float* Y, int64_t ldy,
                     int32_t n_rows, int64_t P, const int32_t* rowptr, const int32_t* col,
                     const float* val, hipStream_t s) {

@@ -79,6 +79,8 @@ SIGNATURES = {
     "dol_mix_csr_slab_f32": [_ptr, _i64, _i32, _ptr, _i64, _i32, _i64, _ptr, _ptr, _ptr],
     "dol_csr_slab_pack": [_ptr, _ptr, _ptr, _i32, _i32, _i32, _ptr, _ptr, _ptr],
     "dol_dense_to_csr_f32": [_ptr, _i64, _i32, _i32, _ptr, _ptr, _ptr, _i64, _ptr],
+    "dol_bank_alloc": [_i64, _ptr, _ptr],  # (bytes, void** out, int64_t* out): addresses of host words
+    "dol_bank_free": [_ptr, _i64],
 }
 _RESTYPES = {"dol_last_error": ctypes.c_char_p, "dol_admm_dual_workspace_bytes": ctypes.c_int64,
              "dol_admm_ls_round_workspace_bytes": ctypes.c_int64,

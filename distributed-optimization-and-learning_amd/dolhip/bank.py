@@ -21,9 +21,12 @@ from __future__ import annotations
 
 from typing import Dict, Iterable, List, Optional, Sequence, Tuple
 
+import ctypes
+import os
+
 import torch
 
-from . import ops
+from . import _native, ops
 
 Layout = List[Tuple[str, Tuple[int, ...]]]
 
@@ -59,6 +62,47 @@ def row_stride(P: int) -> int:
     return ld
 
 
+class _MappedBlock:
+    """Owner of one dol_bank_alloc block, exposed to torch through
+    __cuda_array_interface__ (the tensor's storage keeps this object alive and
+    frees the block with it)."""
+
+    def __init__(self, rows: int, cols: int, device: torch.device):
+        self.device = device
+        nbytes = max(rows * cols, 1) * 4
+        ptr, mapped = ctypes.c_void_p(), ctypes.c_int64()
+        with torch.cuda.device(device):
+            _native.call("dol_bank_alloc", nbytes, ctypes.addressof(ptr), ctypes.addressof(mapped))
+        self.ptr, self.mapped = int(ptr.value), int(mapped.value)
+        self.__cuda_array_interface__ = {"shape": (rows, cols), "typestr": "<f4", "data": (self.ptr, False),
+                                         "version": 2, "strides": None}
+
+    def __del__(self):
+        if getattr(self, "ptr", 0):
+            try:
+                torch.cuda.synchronize(self.device)  # no kernel may still use the block
+                _native.lib().dol_bank_free(self.ptr, self.mapped)
+            except Exception:  # noqa: BLE001 - interpreter teardown
+                pass
+            self.ptr = 0
+
+
+def device_matrix(rows: int, cols: int, device, zero: bool = False) -> torch.Tensor:
+    """A [rows, cols] fp32 device matrix for bank state.  DOL_BANK_ALLOC=vmm
+    places large ones (>= 1 GiB) in one mapped physical allocation
+    (dol_bank_alloc) instead of the caching allocator's block (an experiment on
+    the "slow allocation" boxes; tools/alloc_probe.hip)."""
+    device = torch.device(device)
+    if (os.environ.get("DOL_BANK_ALLOC") == "vmm" and device.type == "cuda"
+            and rows * cols * 4 >= (1 << 30)):
+        t = torch.as_tensor(_MappedBlock(rows, cols, device), device=device)
+        if zero:
+            t.zero_()
+        return t
+    alloc = torch.zeros if zero else torch.empty
+    return alloc(rows, cols, dtype=torch.float32, device=device)
+
+
 class AgentBank:
     def __init__(self, n_agents: int, layout_or_P, device, ld: Optional[int] = None):
         self.device = torch.device(device)
@@ -88,8 +132,7 @@ class AgentBank:
     def buffer(self, name: str, zero: bool = False) -> torch.Tensor:
         t = self._buf.get(name)
         if t is None:
-            alloc = torch.zeros if zero else torch.empty
-            t = alloc(self.n, self.ld, dtype=torch.float32, device=self.device)
+            t = device_matrix(self.n, self.ld, self.device, zero=zero)
             self._buf[name] = t
         return t
 

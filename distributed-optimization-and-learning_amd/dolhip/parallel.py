@@ -33,7 +33,7 @@ import torch
 import torch.distributed as dist
 
 from . import ops
-from .bank import row_stride
+from .bank import device_matrix, row_stride
 
 # Fail fast instead of hanging: every collective of the engine's
 # process groups is bounded by this timeout.  The reference has no collectives
@@ -121,8 +121,8 @@ class ShardedRing:
         self.prev_rank = (self.rank - 1) % self.world
         self.next_rank = (self.rank + 1) % self.world
         if alloc:
-            self.x = torch.empty(self.n_local, self.ld, dtype=torch.float32, device=self.device)
-            self.y = torch.empty_like(self.x)
+            self.x = device_matrix(self.n_local, self.ld, self.device)
+            self.y = device_matrix(self.n_local, self.ld, self.device)
         self.halo_prev = torch.empty(self.ld, dtype=torch.float32, device=self.device)
         self.halo_next = torch.empty(self.ld, dtype=torch.float32, device=self.device)
         # optional (start, end) timing events recorded around the interior kernel

@@ -445,6 +445,17 @@ int64_t dol_mlp_step_lds_bytes(int32_t B, int32_t h, int32_t c);
  */
 int dol_er_stochastic_f32(float* W, int64_t ldw, int32_t n, float p, uint64_t seed, hipStream_t s);
 
+/*
+ * Device memory for a bank buffer as ONE physical allocation (hipMemCreate)
+ * mapped into a reserved virtual range (hipMemAddressReserve + hipMemMap),
+ * rounded up to the allocation granularity (*mapped_bytes).  Free with
+ * dol_bank_free(ptr, *mapped_bytes).  Host-side, synchronous, not
+ * graph-capturable.  No reference counterpart (the reference keeps one
+ * nn.Module per agent in host memory).
+ */
+int dol_bank_alloc(int64_t bytes, void** ptr, int64_t* mapped_bytes);
+int dol_bank_free(void* ptr, int64_t mapped_bytes);
+
 /* Streaming copy dst = src (n floats): HBM calibration kernel for roofline. */
 int dol_stream_copy_f32(const float* src, float* dst, int64_t n, hipStream_t s);
 

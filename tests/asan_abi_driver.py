@@ -51,6 +51,11 @@ for name, argtypes in _native.SIGNATURES.items():
                 sys.exit(5)
             L.dol_pm_set_stage_order(0)
             continue
+        if name == "dol_bank_free" and mode == "null":  # free(NULL) is a no-op, like free()
+            if rc != 0:
+                print(f"{name}(NULL) gave rc={rc}")
+                sys.exit(6)
+            continue
         if mode in ("null", "neg") and rc != -1:
             print(f"{name} accepted {mode} arguments (rc={rc})")
             sys.exit(3)
