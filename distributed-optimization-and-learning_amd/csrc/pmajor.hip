@@ -56,8 +56,10 @@ constexpr uint32_t kOOB = 0x80000000u;    // a buffer offset past every range: t
 __device__ __forceinline__ void wait_vmcnt(int n) {
   switch (n) {
 #define DOL_VMC(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
+#define DOL_VMC8(N) DOL_VMC(N) DOL_VMC(N + 1) DOL_VMC(N + 2) DOL_VMC(N + 3) DOL_VMC(N + 4) DOL_VMC(N + 5) DOL_VMC(N + 6) DOL_VMC(N + 7)
     DOL_VMC(1) DOL_VMC(2) DOL_VMC(3) DOL_VMC(4) DOL_VMC(5) DOL_VMC(6) DOL_VMC(7)
-    DOL_VMC(8) DOL_VMC(9) DOL_VMC(10) DOL_VMC(11) DOL_VMC(12) DOL_VMC(13) DOL_VMC(14) DOL_VMC(15)
+    DOL_VMC8(8) DOL_VMC8(16) DOL_VMC8(24) DOL_VMC8(32) DOL_VMC8(40) DOL_VMC8(48) DOL_VMC8(56)
+#undef DOL_VMC8
 #undef DOL_VMC
     default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
   }
@@ -248,7 +250,7 @@ __global__ __launch_bounds__(T) void csr_pm_kernel(const float* __restrict__ XT,
                                                    int xw, int sr, int qp_log2, int spt, int64_t n_stages, int nseg,
                                                    const int32_t* __restrict__ rowptr,
                                                    const int32_t* __restrict__ col,
-                                                   const float* __restrict__ val, PmDgd e, int nw) {
+                                                   const float* __restrict__ val, PmDgd e, int nw, int wait_all_stores) {
   constexpr int kDma = SF / 4 / T;  // LDS-DMA instructions per thread per stage
   static_assert(kDma * 4 * T == SF, "a stage is a whole number of DMA rounds");
   extern __shared__ __attribute__((aligned(16))) float img[];  // NBUF x SF
@@ -305,10 +307,15 @@ __global__ __launch_bounds__(T) void csr_pm_kernel(const float* __restrict__ XT,
   for (int k = 0; k < NBUF - 1; ++k)
     if (k < nk) issue(k);
   for (int64_t k = 0; k < nk; ++k) {
-    // retire stage k: younger ops are the stages issued after it and (k >= 1)
-    // the previous stage's spt stores
+    // retire stage k: the ops younger than its DMA are the stages issued after
+    // it and the stores of every stage mixed since it was issued -- min(k,
+    // NBUF - 1) of them (vmcnt retires loads and stores in issue order).  r04:
+    // the count before held one stage's stores, so with NBUF > 2 each stage
+    // also waited for the write acknowledgements of the stores NBUF - 2 stages
+    // back (DOL_PM_WAIT=0 restores it, for measurement).
     const int64_t ahead = std::min<int64_t>(nk - 1, k + NBUF - 2) - k;
-    wait_vmcnt(static_cast<int>((k >= 1 ? kStores * spt : 0) + kDma * ahead));
+    const int64_t st_groups = wait_all_stores ? std::min<int64_t>(k, NBUF - 1) : (k >= 1 ? 1 : 0);
+    wait_vmcnt(static_cast<int>(std::min<int64_t>(63, kStores * spt * st_groups + kDma * ahead)));
     __builtin_amdgcn_s_barrier();  // every wave's share landed; buffer (k-1) % NBUF is free
     if (k + NBUF - 1 < nk) issue(k + NBUF - 1);
     const int64_t p0 = stage_of(k) * sr;
@@ -459,8 +466,9 @@ int mix_csr_pm_impl(const char* nm, const float* XT, int64_t ldx, int32_t x_rows
     const int proc = g_pm_nseg.load(std::memory_order_relaxed);
     int nseg = nseg_req > 0 ? nseg_req : proc > 0 ? proc : env_int("DOL_PM_NSEG", 8);
     if (nseg < 1 || grid % nseg) nseg = 1;
+    static const int wait_mode = env_int("DOL_PM_WAIT", 1);
     hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(grid)), dim3(kT1), lds, s, XT, ldx, x_rows, YT, ldy, n_rows, P,
-                       xw, sr, qp_log2, spt, n_stages, nseg, rowptr, col, val, e, nw);
+                       xw, sr, qp_log2, spt, n_stages, nseg, rowptr, col, val, e, nw, wait_mode);
   };
   using std::integral_constant;
   if (obj >= 0) {  // small geometry only

@@ -25,12 +25,13 @@ def main():
     ap.add_argument("--variants", type=int, nargs="+", default=[1, 2, 3])
     ap.add_argument("--agents", type=int, default=8192)
     ap.add_argument("--params", type=int, default=1 << 20)
+    ap.add_argument("--ld", type=int, default=0, help="row stride in floats (0: ShardedRing's row_stride(P))")
     a = ap.parse_args()
     dev = torch.device("cuda")
     N, P = a.agents, a.params
     wp = torch.rand(N)
     wn = torch.rand(N)
-    ring = ShardedRing(N, P, wp, wn, dev)
+    ring = ShardedRing(N, P, wp, wn, dev, ld=a.ld or None)
     ring.x.normal_()
     X, Y = ring.x, ring.y
 
@@ -53,7 +54,8 @@ def main():
             res[str(v)].append(timed(lambda: ops.mix_ring_steps(X, Y, ring.w_prev, ring.w_next, a.eps, P=P, n_rows=N,
                                                                 variant=v)))
     best = {k: min(v) for k, v in res.items()}
-    print(json.dumps({"eps": a.eps, "agents": N, "params": P, "dma_d": os.environ.get("DOL_RING_DMA_D", "8"),
+    print(json.dumps({"eps": a.eps, "agents": N, "params": P, "ld": X.stride(0),
+                      "dma_d": os.environ.get("DOL_RING_DMA_D", "8"),
                       "ms": res, "best_ms": best,
                       "best_TBps": {k: 2 * N * P * 4 / v / 1e9 for k, v in best.items()}}), flush=True)
 
