@@ -519,11 +519,11 @@ __device__ __forceinline__ void vm_wait() {
 using rsrc_t = __amdgpu_buffer_rsrc_t;
 constexpr uint32_t kOOB = 0x80000000u;  // a buffer offset past every range: the access is dropped
 
-template <int S, int D, int PF, bool INTERIOR, int PROBE = 0>
+template <int S, int D, int PF, bool INTERIOR, int PROBE = 0, bool SYNC = false>
 __device__ __forceinline__ void ring_stream_dma_body(const float* __restrict__ X, int64_t ldx, float* __restrict__ Y,
                                                      int64_t ldy, int64_t c, int n_rows, int r0, int nT,
                                                      const float* __restrict__ wprev,
-                                                     const float* __restrict__ wnext, float* ring) {
+                                                     const float* __restrict__ wnext, float* ring, bool live) {
   static_assert(D == PF || D == 2 * PF, "ring slots are compile-time within a chunk");
   static_assert(2 * D - 2 <= 63, "vmcnt is 6 bits");
   const int nsteps = nT + 2 * S;
@@ -556,7 +556,7 @@ __device__ __forceinline__ void ring_stream_dma_body(const float* __restrict__ X
   };
   const uint32_t voff = static_cast<uint32_t>(c) * 16u;
   auto store = [&](int i, f4 v) {  // output of step i: row r0 + i - 2S when 2S <= i < nsteps, else dropped
-    const bool ok = i >= 2 * S && i < nsteps;
+    const bool ok = live && i >= 2 * S && i < nsteps;
     const uint32_t oob = kOOB + (uint32_t(i + D) << 4);  // distinct dropped addresses: no two dummy stores merge
     const int r = ok ? r0 + i - 2 * S : r0;
     const rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(Y + int64_t(r) * ldy, 0, static_cast<int>(ldy * 4), 0x00020000);
@@ -575,6 +575,9 @@ __device__ __forceinline__ void ring_stream_dma_body(const float* __restrict__ X
   for (int t = 0; t < S; ++t) hA[t] = hB[t] = f4{0.f, 0.f, 0.f, 0.f};
   struct Wn { float v[PF + S]; };
   for (int i0 = 0; i0 < ntot; i0 += PF) {
+    // SYNC: the block's four waves meet once per chunk, so the four 1-KiB pieces
+    // of each row are requested together (raw s_barrier: no vmcnt drain)
+    if constexpr (SYNC) __builtin_amdgcn_s_barrier();
     Wn wp, wn;
     if constexpr (INTERIOR) {
       wp = *reinterpret_cast<const Wn*>(wprev + (r0 - 2 * S + i0));
@@ -612,7 +615,7 @@ __device__ __forceinline__ void ring_stream_dma_body(const float* __restrict__ X
   vm_wait<0>();  // no LDS-DMA may land after the wave's LDS is released
 }
 
-template <int S, int D, int PF, int PROBE = 0>
+template <int S, int D, int PF, int PROBE = 0, bool SYNC = false>
 __global__ __launch_bounds__(kThreads) void ring_stream_dma_kernel(
     const float* __restrict__ X, int64_t ldx, float* __restrict__ Y, int64_t ldy, int n_rows,
     int64_t ncols_v, uint32_t n_col_tiles, const float* __restrict__ wprev,
@@ -630,15 +633,17 @@ __global__ __launch_bounds__(kThreads) void ring_stream_dma_kernel(
     ct = b % nct8;
     r0 = static_cast<int>(b / nct8) * T;
   }
-  if (ct >= n_col_tiles) return;
-  const int64_t c = int64_t(ct) * kThreads + threadIdx.x;
-  if (c >= ncols_v) return;
+  if (ct >= n_col_tiles) return;  // the whole block
+  int64_t c = int64_t(ct) * kThreads + threadIdx.x;
+  const bool live = c < ncols_v;
+  if (!SYNC && !live) return;
+  if (!live) c = ncols_v - 1;  // SYNC: every wave reaches the barriers; a dead lane loads a valid column, stores nothing
   const int nT = min(T, n_rows - r0);
   float* ring = &lds[threadIdx.x >> 6][0][0];
   if (r0 - 2 * S >= 0 && r0 + nT + S + PF <= n_rows)  // every row and weight index in range
-    ring_stream_dma_body<S, D, PF, true, PROBE>(X, ldx, Y, ldy, c, n_rows, r0, nT, wprev, wnext, ring);
+    ring_stream_dma_body<S, D, PF, true, PROBE, SYNC>(X, ldx, Y, ldy, c, n_rows, r0, nT, wprev, wnext, ring, live);
   else
-    ring_stream_dma_body<S, D, PF, false, PROBE>(X, ldx, Y, ldy, c, n_rows, r0, nT, wprev, wnext, ring);
+    ring_stream_dma_body<S, D, PF, false, PROBE, SYNC>(X, ldx, Y, ldy, c, n_rows, r0, nT, wprev, wnext, ring, live);
 }
 
 // ----------------------------------------------------------------------------
@@ -1724,6 +1729,8 @@ int dol_mix_ring_steps_ex_f32(const float* X, int64_t ldx, float* Y, int64_t ldy
   };
   // variant 3: ring_stream_dma_kernel, D-row LDS-DMA ring per wave (DOL_RING_DMA_D 8 / 16)
   static const int dma_d = [] { const char* e = getenv("DOL_RING_DMA_D"); return e ? atoi(e) : 8; }();
+  // DOL_RING_DMA_SYNC=1: one raw barrier per 8 steps keeps a block's waves on the same rows
+  static const int dma_sync = [] { const char* e = getenv("DOL_RING_DMA_SYNC"); return e ? atoi(e) : 0; }();
   // DOL_RING_DMA_ORDER: 0 = XCD-aware row-tile order, 1 = column tile fastest (sweep)
   static const int dma_order = [] { const char* e = getenv("DOL_RING_DMA_ORDER"); return e ? atoi(e) : 0; }();
   auto go_stream_dma = [&](auto steps_c, int T) {
@@ -1742,7 +1749,10 @@ int dol_mix_ring_steps_ex_f32(const float* X, int64_t ldx, float* Y, int64_t ldy
         return check_launch("dol_mix_ring_steps_f32");
       }
     }
-    if (dma_d == 16)
+    if (dma_sync)
+      hipLaunchKernelGGL((ring_stream_dma_kernel<S, 8, 8, 0, true>), dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, s,
+                         X, ldx, Y, ldy, n_rows, nv, nct, w_prev, w_next, static_cast<uint32_t>(nrt), T, dma_order);
+    else if (dma_d == 16)
       hipLaunchKernelGGL((ring_stream_dma_kernel<S, 16, 8>), dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, s, X,
                          ldx, Y, ldy, n_rows, nv, nct, w_prev, w_next, static_cast<uint32_t>(nrt), T, dma_order);
     else

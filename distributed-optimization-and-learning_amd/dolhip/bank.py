@@ -87,14 +87,20 @@ class _MappedBlock:
             self.ptr = 0
 
 
+MAPPED_MIN_BYTES = 1 << 30
+
+
 def device_matrix(rows: int, cols: int, device, zero: bool = False) -> torch.Tensor:
-    """A [rows, cols] fp32 device matrix for bank state.  DOL_BANK_ALLOC=vmm
-    places large ones (>= 1 GiB) in one mapped physical allocation
-    (dol_bank_alloc) instead of the caching allocator's block (an experiment on
-    the "slow allocation" boxes; tools/alloc_probe.hip)."""
+    """A [rows, cols] fp32 device matrix for bank state.  Large ones (>= 1 GiB)
+    are ONE mapped physical allocation (dol_bank_alloc: hipMemCreate +
+    hipMemMap) instead of a caching-allocator block: the ring round at 8192 x
+    2^20 ran 10.93-10.96 ms on such buffers against 11.15-11.17 on hipMalloc'd
+    ones, alternating in one process (tools/alloc_probe.hip,
+    profiles/r04e_alloc_probe.jsonl).  DOL_BANK_ALLOC=torch keeps torch's
+    allocator for everything."""
     device = torch.device(device)
-    if (os.environ.get("DOL_BANK_ALLOC") == "vmm" and device.type == "cuda"
-            and rows * cols * 4 >= (1 << 30)):
+    if (os.environ.get("DOL_BANK_ALLOC", "vmm") == "vmm" and device.type == "cuda"
+            and rows * cols * 4 >= MAPPED_MIN_BYTES):
         t = torch.as_tensor(_MappedBlock(rows, cols, device), device=device)
         if zero:
             t.zero_()
