@@ -315,7 +315,9 @@ def _events_ms(fn, reps: int) -> float:
     return s.elapsed_time(e) / reps
 
 
-RING_STEPS_KERNELS = {1: "ring_steps_kernel (register tiles)", 2: "ring_stream_kernel", 3: "ring_stream_dma_kernel"}
+RING_STEPS_KERNELS = {1: "ring_steps_kernel (register tiles)", 2: "ring_stream_kernel", 3: "ring_stream_dma_kernel",
+                      4: "ring_stream_dma_kernel (block-synchronised)",
+                      5: "ring_stream_dma_kernel (64-row tiles, column-tile-fastest sweep)"}
 
 
 def fedlcon_eps_round(device, ring, N: int, P: int, eps: int = 5, reps: int = 10):

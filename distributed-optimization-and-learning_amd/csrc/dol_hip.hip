@@ -55,7 +55,7 @@ using dol::g_err;
 
 constexpr int kThreads = 256;            // 4 waves of 64
 constexpr int64_t kMaxBlocks = int64_t(1) << 24;
-constexpr int kRingStepsVariants = 3;  // highest dol_mix_ring_steps_ex_f32 variant
+constexpr int kRingStepsVariants = 5;  // highest dol_mix_ring_steps_ex_f32 variant
 
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
@@ -1662,7 +1662,7 @@ static std::atomic<int> g_ring_steps_variant{0};
 
 int dol_ring_steps_set_variant(int32_t variant) {
   if (variant < 0 || variant > kRingStepsVariants)
-    return fail(DOL_EINVAL, "dol_ring_steps_set_variant: variant %d outside 0 (default) / 1 (tiles) / 2 (stream) / 3 (stream, LDS-DMA)", variant);
+    return fail(DOL_EINVAL, "dol_ring_steps_set_variant: variant %d outside 0 (default) / 1 (tiles) / 2 (stream) / 3-5 (LDS-DMA stream: plain, synchronised, sweep)", variant);
   const int prev = g_ring_steps_variant.exchange(variant, std::memory_order_relaxed);
   g_err[0] = '\0';
   return prev;
@@ -1679,7 +1679,7 @@ int dol_mix_ring_steps_ex_f32(const float* X, int64_t ldx, float* Y, int64_t ldy
                               int32_t variant, hipStream_t s) {
   DOL_DIMS_OK("dol_mix_ring_steps_f32", ldx, ldy, P);
   if (variant < 0 || variant > kRingStepsVariants)
-    return fail(DOL_EINVAL, "dol_mix_ring_steps_ex_f32: variant %d outside 0 (process setting) / 1 (tiles) / 2 (stream) / 3 (stream, LDS-DMA)", variant);
+    return fail(DOL_EINVAL, "dol_mix_ring_steps_ex_f32: variant %d outside 0 (process setting) / 1 (tiles) / 2 (stream) / 3-5 (LDS-DMA stream: plain, synchronised, sweep)", variant);
   if (n_rows < 0 || P < 0 || steps < 0) return fail(DOL_EINVAL, "dol_mix_ring_steps_f32: negative size");
   if (n_rows == 0 || P == 0) { g_err[0] = '\0'; return DOL_OK; }
   if (!X || !Y || !w_prev || !w_next) return fail(DOL_EINVAL, "dol_mix_ring_steps_f32: null pointer");
@@ -1703,7 +1703,9 @@ int dol_mix_ring_steps_ex_f32(const float* X, int64_t ldx, float* Y, int64_t ldy
   // times both on the buffers in use and keeps the faster (dol_ring_steps_set_variant).
   static const int stream_env = [] { const char* e = getenv("DOL_RING_STREAM"); return e ? atoi(e) : 0; }();
   const int v = variant != 0 ? variant : g_ring_steps_variant.load(std::memory_order_relaxed);
-  const int stream = v == 0 ? stream_env : (v == 2 ? 1 : v == 3 ? 3 : 0);
+  // stream: 0 register tiles, 1 register stream, 3 / 4 / 5 LDS-DMA stream
+  // (plain / block-synchronised / column-tile-fastest sweep of 64-row tiles)
+  const int stream = v == 0 ? stream_env : (v == 2 ? 1 : v >= 3 ? v : 0);
   static const int stream_t = [] { const char* e = getenv("DOL_RING_STREAM_T"); return e ? atoi(e) : 1024; }();
   static const int stream_pf = [] { const char* e = getenv("DOL_RING_STREAM_PF"); return e ? atoi(e) : 8; }();
   static const int stream_nt = [] { const char* e = getenv("DOL_RING_STREAM_NT"); return e ? atoi(e) : 1; }();
@@ -1735,6 +1737,9 @@ int dol_mix_ring_steps_ex_f32(const float* X, int64_t ldx, float* Y, int64_t ldy
   static const int dma_order = [] { const char* e = getenv("DOL_RING_DMA_ORDER"); return e ? atoi(e) : 0; }();
   auto go_stream_dma = [&](auto steps_c, int T) {
     constexpr int S = decltype(steps_c)::value;
+    const bool sync = stream == 4 || dma_sync;
+    const int order = stream == 5 ? 1 : dma_order;
+    if (stream == 5) T = 64;
     const int64_t nv = P / 4;
     const uint32_t nct = static_cast<uint32_t>(cdiv(nv, kThreads));
     const int64_t nrt = cdiv(n_rows, T);
@@ -1745,23 +1750,23 @@ int dol_mix_ring_steps_ex_f32(const float* X, int64_t ldx, float* Y, int64_t ldy
     if constexpr (S == 5) {
       if (dma_probe == 1) {
         hipLaunchKernelGGL((ring_stream_dma_kernel<S, 8, 8, 1>), dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, s,
-                           X, ldx, Y, ldy, n_rows, nv, nct, w_prev, w_next, static_cast<uint32_t>(nrt), T, dma_order);
+                           X, ldx, Y, ldy, n_rows, nv, nct, w_prev, w_next, static_cast<uint32_t>(nrt), T, order);
         return check_launch("dol_mix_ring_steps_f32");
       }
     }
-    if (dma_sync)
+    if (sync)
       hipLaunchKernelGGL((ring_stream_dma_kernel<S, 8, 8, 0, true>), dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, s,
-                         X, ldx, Y, ldy, n_rows, nv, nct, w_prev, w_next, static_cast<uint32_t>(nrt), T, dma_order);
+                         X, ldx, Y, ldy, n_rows, nv, nct, w_prev, w_next, static_cast<uint32_t>(nrt), T, order);
     else if (dma_d == 16)
       hipLaunchKernelGGL((ring_stream_dma_kernel<S, 16, 8>), dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, s, X,
-                         ldx, Y, ldy, n_rows, nv, nct, w_prev, w_next, static_cast<uint32_t>(nrt), T, dma_order);
+                         ldx, Y, ldy, n_rows, nv, nct, w_prev, w_next, static_cast<uint32_t>(nrt), T, order);
     else
       hipLaunchKernelGGL((ring_stream_dma_kernel<S, 8, 8>), dim3(static_cast<unsigned>(grid)), dim3(kThreads), 0, s, X,
-                         ldx, Y, ldy, n_rows, nv, nct, w_prev, w_next, static_cast<uint32_t>(nrt), T, dma_order);
+                         ldx, Y, ldy, n_rows, nv, nct, w_prev, w_next, static_cast<uint32_t>(nrt), T, order);
     return check_launch("dol_mix_ring_steps_f32");
   };
   auto go_stream = [&](auto steps_c, int T) {
-    if (stream == 3) return go_stream_dma(steps_c, T);
+    if (stream >= 3) return go_stream_dma(steps_c, T);
     if (stream_pf == 16) return go_stream_pf(steps_c, T, std::integral_constant<int, 16>{});
     if (stream_pf == 4) return go_stream_pf(steps_c, T, std::integral_constant<int, 4>{});
     return go_stream_pf(steps_c, T, std::integral_constant<int, 8>{});
@@ -1771,7 +1776,7 @@ int dol_mix_ring_steps_ex_f32(const float* X, int64_t ldx, float* Y, int64_t ldy
     constexpr int S = decltype(steps_c)::value, R = decltype(r_c)::value;
     // the stream kernels wrap at most once (PF <= 16); the LDS-DMA one's buffer
     // stores address a row in 32 bits
-    if (stream && n_rows >= 2 * S + 16 + 1 && (stream != 3 || ldy * 4 < (int64_t(1) << 31))) {
+    if (stream && n_rows >= 2 * S + 16 + 1 && (stream < 3 || ldy * 4 < (int64_t(1) << 31))) {
       return go_stream(steps_c, stream_t >= 64 ? stream_t : 1024);
     }
     using V = typename decltype(v_c)::type;

@@ -541,13 +541,29 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd_kernel(MlpArgs a, float* __r
     auto ok = [&](int i) { return o0 + i * kThreads + t < c * h; };
     auto idx = [&](int i) { return oW2 + (ok(i) ? o0 + i * kThreads + t : 0); };
     if (o0 > 0) pb.load(a, wrow, mrow, arow, idx);
+    if (kThreads % h == 0) {  // k = t % h for all 8 outputs: one H read per sample serves them all (r04)
+      const int k = t % h;
+      int jj[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int o = ok(i) ? o0 + i * kThreads + t : 0;
-      const int j = o / h, k = o % h;
-      float s = 0.0f;
-      for (int b = 0; b < B; ++b) s = s + Zs[b * c + j] * Hs[b * hp + k];
-      g[i] = s;
+      for (int i = 0; i < 8; ++i) {
+        jj[i] = ok(i) ? (o0 + i * kThreads + t) / h : 0;
+        g[i] = 0.0f;
+      }
+      for (int b = 0; b < B; ++b) {  // per output the same products, summed over b ascending
+        const float hv = Hs[b * hp + k];
+        const float* zr = Zs + b * c;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) g[i] = g[i] + zr[jj[i]] * hv;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int o = ok(i) ? o0 + i * kThreads + t : 0;
+        const int j = o / h, k = o % h;
+        float s = 0.0f;
+        for (int b = 0; b < B; ++b) s = s + Zs[b * c + j] * Hs[b * hp + k];
+        g[i] = s;
+      }
     }
     if (o0 == 0) pw2.commit(a, wrow, grow, mrow, g, idx, ok);
     else pb.commit(a, wrow, grow, mrow, g, idx, ok);
@@ -563,13 +579,38 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd_kernel(MlpArgs a, float* __r
   __syncthreads();
 
   // ---- B2b: dZ1 = (dZ2 W2) * [H > 0], in place over H
+  if (kThreads % h == 0 && B * h <= 16 * kThreads) {
+    // k = t % h for every output of this thread: one W2 read per class serves
+    // up to 16 samples (r04; per output the same products, j ascending)
+    const int k = t % h, b0 = t / h, bs = kThreads / h;
+    float sm[16];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) sm[m] = 0.0f;
+    for (int j = 0; j < c; ++j) {
+      const float w2 = W2s[j * hp + k];
+#pragma unroll
+      for (int m = 0; m < 16; ++m) {
+        const int b = b0 + m * bs;
+        if (b < B) sm[m] = sm[m] + Zs[b * c + j] * w2;
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      const int b = b0 + m * bs;
+      if (b < B) {
+        float* hv = Hs + b * hp + k;
+        *hv = (*hv > 0.0f) ? sm[m] : 0.0f;
+      }
+    }
+  } else {
 #pragma unroll 4
-  for (int o = t; o < B * h; o += kThreads) {
-    const int b = o / h, k = o % h;
-    float s = 0.0f;
-    for (int j = 0; j < c; ++j) s = s + Zs[b * c + j] * W2s[j * hp + k];
-    float* hv = Hs + b * hp + k;
-    *hv = (*hv > 0.0f) ? s : 0.0f;
+    for (int o = t; o < B * h; o += kThreads) {
+      const int b = o / h, k = o % h;
+      float s = 0.0f;
+      for (int j = 0; j < c; ++j) s = s + Zs[b * c + j] * W2s[j * hp + k];
+      float* hv = Hs + b * hp + k;
+      *hv = (*hv > 0.0f) ? s : 0.0f;
+    }
   }
   __syncthreads();
 

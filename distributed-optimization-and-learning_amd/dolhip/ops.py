@@ -149,6 +149,7 @@ def tune_pm_stage_order(run, candidates=(8, 16, 32), reps: int = 3) -> dict:
 
 def ring_steps_variant(variant: int) -> int:
     """Kernel of mix_ring_steps for this process: 1 register tiles, 2 streaming,
+    3 / 4 / 5 streaming by LDS-DMA (plain / block-synchronised / 64-row sweep),
     0 default; returns the previous setting (dol_ring_steps_set_variant)."""
     rc = _native.lib().dol_ring_steps_set_variant(int(variant))
     if rc < 0:
@@ -203,7 +204,7 @@ def tune_ring_steps_variant(run, reps: int = 3) -> dict:
 # after the memory is reused can only cost speed.  DOL_AUTOTUNE=0 turns it off
 # (every call then takes the library default).
 # ---------------------------------------------------------------------------
-RING_STEPS_VARIANTS = (1, 2, 3)
+RING_STEPS_VARIANTS = (1, 2, 3, 4, 5)
 PM_STAGE_ORDERS = (8, 16, 32)
 AUTOTUNE_MIN_BYTES = 1 << 30  # below this one pass is too short to be worth timing
 AUTOTUNE_REPS = 3

@@ -95,9 +95,12 @@ int dol_pm_set_stage_order(int32_t nseg);
 
 /*
  * Kernel of dol_mix_ring_steps_f32 for this process: 1 = register tiles
- * (ring_steps_kernel), 2 = streaming (ring_stream_kernel, used when n_rows >=
- * 2 * steps + 17), 0 = the default (DOL_RING_STREAM, else tiles).  Same bits
- * either way.  Returns the previous setting, or DOL_EINVAL outside [0, 2].
+ * (ring_steps_kernel), 2 = streaming (ring_stream_kernel), 3 / 4 / 5 =
+ * streaming with the rows arriving by LDS-DMA (ring_stream_dma_kernel: plain,
+ * block-synchronised once per 8 rows, 64-row tiles in column-tile-fastest
+ * order); the streaming kernels need n_rows >= 2 * steps + 17 (else tiles).
+ * 0 = the default (DOL_RING_STREAM, else tiles).  Same bits for every
+ * variant.  Returns the previous setting, or DOL_EINVAL outside [0, 5].
  * No reference counterpart (a launch choice of this implementation).  Atomic,
  * like dol_pm_set_stage_order; dol_mix_ring_steps_ex_f32 takes it per call.
  */

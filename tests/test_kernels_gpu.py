@@ -589,7 +589,7 @@ def test_prox_grad_term_vs_oracle(admm, extra, gpu):
     assert bits_equal(gd[:, :P].cpu().numpy(), oracle.prox_grad(g, w, th, al, 0.1))
 
 
-@pytest.fixture(params=list(ops.RING_STEPS_VARIANTS), ids=lambda v: {1: "tiles", 2: "stream", 3: "dma"}[v])
+@pytest.fixture(params=list(ops.RING_STEPS_VARIANTS), ids=lambda v: {1: "tiles", 2: "stream", 3: "dma", 4: "dmasync", 5: "dmasweep"}[v])
 def ring_variant(request):
     """dol_ring_steps_set_variant for the test, restored after it."""
     prev = ops.ring_steps_variant(request.param)

@@ -65,8 +65,8 @@ def test_pm_stage_order_setter():
     assert L.dol_pm_set_stage_order(-1) == -1 and b"outside" in L.dol_last_error()
     prev = L.dol_pm_set_stage_order(32)
     assert L.dol_pm_set_stage_order(prev) == 32
-    assert L.dol_ring_steps_set_variant(4) == -1 and b"outside" in L.dol_last_error()
-    assert L.dol_ring_steps_set_variant(3) == 0 and L.dol_ring_steps_set_variant(0) == 3  # the LDS-DMA stream
+    assert L.dol_ring_steps_set_variant(6) == -1 and b"outside" in L.dol_last_error()
+    assert L.dol_ring_steps_set_variant(5) == 0 and L.dol_ring_steps_set_variant(0) == 5  # the LDS-DMA sweep
     prev = L.dol_ring_steps_set_variant(2)
     assert L.dol_ring_steps_set_variant(prev) == 2
 
