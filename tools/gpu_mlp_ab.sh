@@ -6,7 +6,7 @@ OUT=gpurun_out/${OUT:-mlp_ab}
 mkdir -p "$OUT"
 for v in ${VARIANTS:-DOL_MLP_DW1_CHAINS=1 DOL_MLP_DW1_CHAINS=2}; do
   env $(echo $v | tr , " ") timeout -k 10 300 python -u -m pytest tests/test_mlp_gpu.py -k "${PYTEST_K:-not bit_identical}" -x -q --timeout 200 --timeout-method thread > "$OUT/pytest_$v.log" 2>&1
-  rc=$?; echo "$v pytest rc=$rc $(tail -1 "$OUT/pytest_$v.log")"; [ $rc -eq 0 ] || exit $rc
+  rc=$?; echo "$v pytest rc=$rc $(tail -1 "$OUT/pytest_$v.log")"; [ $rc -eq 0 ] || [ $rc -eq 5 ] || exit $rc
 done
 for rep in ${REPS:-1 2 3}; do
   for v in ${VARIANTS:-DOL_MLP_DW1_CHAINS=1 DOL_MLP_DW1_CHAINS=2}; do
