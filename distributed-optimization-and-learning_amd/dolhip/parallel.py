@@ -345,6 +345,12 @@ class AgentColumnTranspose:
         # columns sends n_local x P and receives N x Pc floats, and back
         self._buf_rows = torch.empty(max(self.n_local * P, 1), dtype=torch.float32, device=self.device)
         self._buf_cols = torch.empty(max(self.N * self.Pc, 1), dtype=torch.float32, device=self.device)
+        # r04: when the column block is a whole number of 16-B pieces, the mix reads
+        # the received [N, Pc] block in place and writes the send buffer of the
+        # way back (two staging copies fewer per round: direct=True)
+        self.direct = self.world > 1 and self.Pc > 0 and self.Pc % 4 == 0
+        self._buf_cols2 = (torch.empty(self.N * self.Pc, dtype=torch.float32, device=self.device)
+                           if self.direct else None)
 
     def set_plan(self, plan) -> None:
         if (plan.n_rows, plan.n_cols) != (self.N, self.N):
@@ -368,11 +374,7 @@ class AgentColumnTranspose:
         if self.world == 1:
             self.cols[:, :P].copy_(rows[:, :P])
             return
-        send = self._buf_rows[:n * P]
-        off = 0
-        for a, b in self.col_bounds:  # to rank q: my rows x its columns
-            send[off:off + n * (b - a)].view(n, b - a).copy_(rows[:, a:b])
-            off += n * (b - a)
+        send = self._pack_rows(rows)
         recv = self._buf_cols[:self.N * self.Pc]
         self._all_to_all(send, recv, [n * (b - a) for a, b in self.col_bounds],
                          [(h - l) * self.Pc for l, h in self.row_bounds])
@@ -390,24 +392,55 @@ class AgentColumnTranspose:
         recv = self._buf_rows[:n * P]
         self._all_to_all(send, recv, [(h - l) * self.Pc for l, h in self.row_bounds],
                          [n * (b - a) for a, b in self.col_bounds])
+        self._unpack_rows(recv, rows)
+
+    def _pack_rows(self, rows: torch.Tensor) -> torch.Tensor:
+        P, n = self.P, self.n_local
+        send = self._buf_rows[:n * P]
         off = 0
+        for a, b in self.col_bounds:  # to rank q: my rows x its columns
+            send[off:off + n * (b - a)].view(n, b - a).copy_(rows[:, a:b])
+            off += n * (b - a)
+        return send
+
+    def _unpack_rows(self, recv: torch.Tensor, rows: torch.Tensor) -> None:
+        n, off = self.n_local, 0
         for a, b in self.col_bounds:  # from rank q: my agents x its columns
             w = b - a
             rows[:, a:b].copy_(recv[off:off + n * w].view(n, w))
             off += n * w
 
+    def _apply_block(self, X: torch.Tensor, Y: torch.Tensor) -> None:
+        if self._apply is not None:
+            self._apply(X, Y, P=self.Pc)
+        else:
+            if self.plan is None:
+                raise RuntimeError("AgentColumnTranspose.mix: set_plan() first")
+            self.plan.apply(X, Y, P=self.Pc)
+
     def mix(self, rows: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """One Jacobi round Y = W X for this rank's agents (out may be rows' own
         storage: the column block is a separate buffer)."""
         out = rows if out is None else out
+        if self.direct:
+            # rows -> send (pack) -> all_to_all -> [N, Pc] block (agents in rank =
+            # agent order) -> mix in place into the way-back send buffer ->
+            # all_to_all -> unpack: the same elements and the same arithmetic as
+            # the staged path below, without its two block copies
+            n, N, Pc = self.n_local, self.N, self.Pc
+            recv = self._buf_cols[:N * Pc]
+            self._all_to_all(self._pack_rows(rows), recv, [n * (b - a) for a, b in self.col_bounds],
+                             [(h - l) * Pc for l, h in self.row_bounds])
+            Y = self._buf_cols2[:N * Pc]
+            self._apply_block(recv.view(N, Pc), Y.view(N, Pc))
+            back = self._buf_rows[:n * self.P]
+            self._all_to_all(Y, back, [(h - l) * Pc for l, h in self.row_bounds],
+                             [n * (b - a) for a, b in self.col_bounds])
+            self._unpack_rows(back, out)
+            return out
         self.to_columns(rows)
         if self.Pc > 0:
-            if self._apply is not None:
-                self._apply(self.cols, self.cols_out, P=self.Pc)
-            else:
-                if self.plan is None:
-                    raise RuntimeError("AgentColumnTranspose.mix: set_plan() first")
-                self.plan.apply(self.cols, self.cols_out, P=self.Pc)
+            self._apply_block(self.cols, self.cols_out)
         self.from_columns(out)
         return out
 
