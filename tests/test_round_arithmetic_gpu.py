@@ -61,8 +61,9 @@ class Pin:
             torch.cuda.synchronize()
             a1, r = oracle.admm_dual(A, W, TH, np.float32(rho))
             assert oracle.bits_equal(_host(alpha[:, :P]), a1), "update_duals"
-            if resid_sq is not None:
-                np.testing.assert_allclose(resid_sq[:alpha.shape[0]].cpu().numpy(), r, rtol=1e-12)
+            if resid_sq is not None:  # the fp64 diagnostic: both sums fixed-order, in different orders;
+                # over P = 1.66M squares the orders differ by up to ~P * 2^-53 relative (observed 1.6e-12)
+                np.testing.assert_allclose(resid_sq[:alpha.shape[0]].cpu().numpy(), r, rtol=1e-9)
             self._count(name)
 
         def ordered_mean(W, order, out=None, P=None):
