@@ -188,25 +188,43 @@ print("ok")
 """
 
 
-def test_fused_one_kernel_step_bit_identical(gpu, tmp_path):
-    """The one-kernel step with W1 resident in registers (DOL_MLP_FUSED=1, read
-    once per process: run in children) gives the same parameters, momentum,
-    gradients and losses as the forward + dW1 kernels, bit for bit: d with and
-    without a partial last chunk, B < 32, plain and momentum SGD, first steps,
-    write_grad, and a shape outside the fused path (falls back)."""
+_STEP_PATHS = {  # env of each alternative launch path (read once per process: run in children)
+    "base": dict(DOL_MLP_FUSED="0", DOL_MLP_SPLIT_FWD="0", DOL_MLP_F1_TILES="0"),
+    "fused": dict(DOL_MLP_FUSED="1"),
+    "split": dict(DOL_MLP_SPLIT_FWD="1"),
+    "f1tiles4": dict(DOL_MLP_F1_TILES="4"),
+    "f1tiles5": dict(DOL_MLP_F1_TILES="5"),
+}
+
+
+def _run_step_child(root, tmp_path, name):
     import os
     import subprocess
     import sys
+    f = str(tmp_path / f"{name}.pt")
+    env = dict(os.environ, **{k: "0" for k in _STEP_PATHS["base"]})
+    env.update(_STEP_PATHS[name])
+    r = subprocess.run([sys.executable, "-c", _FUSED_CHILD, root,
+                        os.path.join(root, "distributed-optimization-and-learning_amd"), f],
+                       env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
+    return torch.load(f, weights_only=True)
+
+
+@pytest.mark.parametrize("path", ["fused", "split", "f1tiles4", "f1tiles5"])
+def test_step_paths_bit_identical(path, gpu, tmp_path):
+    """Each alternative launch path of the step gives the same parameters,
+    momentum, gradients and losses as the default forward + dW1 kernels, bit
+    for bit: the one-kernel step with W1 resident in registers
+    (DOL_MLP_FUSED=1), F1 as its own per-agent kernel (DOL_MLP_SPLIT_FWD=1)
+    and F1 per (agent, h-tile) single-wave workgroups (DOL_MLP_F1_TILES=NS),
+    each followed by the per-agent tail.  Cases: d with and without a partial
+    last chunk, B < 32, plain and momentum SGD, first steps, write_grad, and a
+    shape outside the alternative path (B = 33: falls back)."""
+    import os
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    res = {}
-    for v in ("0", "1"):
-        f = str(tmp_path / f"fused{v}.pt")
-        env = dict(os.environ, DOL_MLP_FUSED=v)
-        r = subprocess.run([sys.executable, "-c", _FUSED_CHILD, root,
-                            os.path.join(root, "distributed-optimization-and-learning_amd"), f],
-                           env=env, capture_output=True, text=True, timeout=240)
-        assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
-        res[v] = torch.load(f, weights_only=True)
-    assert res["0"].keys() == res["1"].keys()
-    for k, t in res["0"].items():
-        assert torch.equal(t, res["1"][k]), k
+    base = _run_step_child(root, tmp_path, "base")
+    alt = _run_step_child(root, tmp_path, path)
+    assert base.keys() == alt.keys()
+    for k, t in base.items():
+        assert torch.equal(t, alt[k]), k
