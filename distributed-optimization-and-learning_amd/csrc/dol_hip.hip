@@ -19,6 +19,8 @@
 #include <stdarg.h>
 #include <algorithm>
 #include <atomic>
+#include <mutex>
+#include <unordered_map>
 #include <type_traits>
 
 #include "../../include/dol_hip.h"
@@ -1462,6 +1464,9 @@ int dol_version(void) { return 100; }
 
 const char* dol_last_error(void) { return g_err; }
 
+static std::mutex g_bank_mu;  // dol_bank_alloc's live blocks: VA -> physical handle
+static std::unordered_map<void*, hipMemGenericAllocationHandle_t> g_bank_handles;
+
 // A bank buffer as ONE physical allocation (hipMemCreate) mapped into a
 // reserved VA range, instead of whatever hipMalloc's suballocator returns
 // (tools/alloc_probe.hip measures the ring round on both).
@@ -1493,14 +1498,18 @@ int dol_bank_alloc(int64_t bytes, void** ptr, int64_t* mapped_bytes) {
     (void)hipMemRelease(h);
     return fail(-static_cast<int>(e), "dol_bank_alloc: hipMemMap: %s", hipGetErrorString(e));
   }
-  (void)hipMemRelease(h);  // the mapping keeps the memory until it is unmapped
   hipMemAccessDesc acc{};
   acc.location = prop.location;
   acc.flags = hipMemAccessFlagsProtReadWrite;
   if ((e = hipMemSetAccess(va, size, &acc, 1)) != hipSuccess) {
     (void)hipMemUnmap(va, size);
     (void)hipMemAddressFree(va, size);
+    (void)hipMemRelease(h);
     return fail(-static_cast<int>(e), "dol_bank_alloc: hipMemSetAccess: %s", hipGetErrorString(e));
+  }
+  {  // the handle lives until dol_bank_free has unmapped the range (create, map ... unmap, release)
+    std::lock_guard<std::mutex> lk(g_bank_mu);
+    g_bank_handles[va] = h;
   }
   *ptr = va;
   *mapped_bytes = static_cast<int64_t>(size);
@@ -1511,8 +1520,17 @@ int dol_bank_alloc(int64_t bytes, void** ptr, int64_t* mapped_bytes) {
 int dol_bank_free(void* ptr, int64_t mapped_bytes) {
   if (!ptr) return DOL_OK;
   if (mapped_bytes <= 0 || mapped_bytes > 8 * dol::kMaxDim) return fail(DOL_EINVAL, "dol_bank_free: bad size");
+  hipMemGenericAllocationHandle_t h{};
+  {
+    std::lock_guard<std::mutex> lk(g_bank_mu);
+    auto it = g_bank_handles.find(ptr);
+    if (it == g_bank_handles.end()) return fail(DOL_EINVAL, "dol_bank_free: %p is not a dol_bank_alloc block", ptr);
+    h = it->second;
+    g_bank_handles.erase(it);
+  }
   hipError_t e = hipMemUnmap(ptr, static_cast<size_t>(mapped_bytes));
   if (e == hipSuccess) e = hipMemAddressFree(ptr, static_cast<size_t>(mapped_bytes));
+  if (e == hipSuccess) e = hipMemRelease(h);
   if (e != hipSuccess) return fail(-static_cast<int>(e), "dol_bank_free: %s", hipGetErrorString(e));
   g_err[0] = '\0';
   return DOL_OK;

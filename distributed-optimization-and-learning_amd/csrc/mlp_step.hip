@@ -159,6 +159,37 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
   }
 }
 
+// global -> LDS copy of n floats by the workgroup, N loads in flight per thread
+// (r04): a plain strided loop waits one memory round trip per iteration --
+// the tail of mlp_fwd_kernel PH 2 spent ~16 of them loading H
+template <int N, class Src, class Dst>
+__device__ __forceinline__ void lds_fill(int n, Src src, Dst dst) {
+  const int t = threadIdx.x;
+  for (int o0 = 0; o0 < n; o0 += N * kThreads) {
+    float v[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int o = o0 + i * kThreads + t;
+      v[i] = src(o < n ? o : 0);  // unconditional, from a valid address: no branch per load
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int o = o0 + i * kThreads + t;
+      if (o < n) dst(o, v[i]);
+    }
+  }
+}
+
+// workgroup barrier for LDS traffic only (r04): __syncthreads() also drains
+// vmcnt, so every barrier after a batch of parameter stores (or with LDS-DMA
+// chunks in flight) waited a full HBM round trip; no barrier in these kernels
+// orders global memory between threads
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 constexpr int kStages = 3;  // default F1 LDS-DMA pipeline depth (NS - 1 chunks in flight during the MFMAs)
 
 // LDS layout of mlp_fwd_kernel (floats): [ union: F1 staging | Hs, W2s, Zs ] [ b1s, b2s, ls ] [ ys ];
@@ -307,7 +338,7 @@ __device__ __forceinline__ void mlp_fused_dw1(const MlpArgs& a, const f4 (&wres)
 // floats per lane: the agent's 128 x d W1 lives in the CU's register file), so
 // B1 + the W1 update run on the resident W1 and W1 is read from HBM once, not
 // twice; see mlp_fused_dw1 above.  Bit-identical to 0 + mlp_dw1_kernel
-// (tests/test_mlp_gpu.py::test_fused_one_kernel_step_bit_identical), opt-in
+// (tests/test_mlp_gpu.py::test_step_paths_bit_identical), opt-in
 // (DOL_MLP_FUSED=1): see the measurement at the dispatch below.
 template <int NT, int UPD, bool TH, bool AL, int NS = kStages, int PH = 0, int NK = 0>
 __global__ __launch_bounds__(kThreads) void mlp_fwd_kernel(MlpArgs a, float* __restrict__ ws) {
@@ -359,7 +390,7 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd_kernel(MlpArgs a, float* __r
   }
   if constexpr (PH == 0 || PH == 3)
     for (int i = t; i < h; i += kThreads) b1s[i] = wrow[ob1 + i];
-  if constexpr (PH != 1) __syncthreads();  // PH 1: the staging is the whole LDS (b1 read from memory below)
+  if constexpr (PH != 1) lds_barrier();  // PH 1: the staging is the whole LDS (b1 read from memory below)
   float* wsa = ws + int64_t(agent) * B * h;  // H (PH 1 -> 2), then dZ1 for mlp_dw1_kernel
   // ---- F1: Z1^T tiles (32 h x 32 b) on MFMA, K = d in chunks of 32
   const int nht = h / 32, nbt = (B + 31) / 32;
@@ -414,7 +445,7 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd_kernel(MlpArgs a, float* __r
   f4 wres[PH == 3 ? NK - KL : 1][4];
   const int i0_b1 = UPD == 3 ? 0 : PH == 3 ? 4 : h / 32;  // PH 3's B1 chunks: momentum rows (UPD 3) + X rows, or X rows only
   if constexpr (PH == 2) {  // H from the F1 kernel
-    for (int o = t; o < B * h; o += kThreads) Hs[(o / h) * hp + (o % h)] = wsa[o];
+    lds_fill<16>(B * h, [&](int o) { return wsa[o]; }, [&](int o, float v) { Hs[(o / h) * hp + (o % h)] = v; });
   } else {
 
   f32x16 acc[NT];
@@ -433,7 +464,7 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd_kernel(MlpArgs a, float* __r
         if (kc * 32 + 4 * ((lane & 7) ^ (lane >> 3)) >= d)
           *reinterpret_cast<f4*>(const_cast<float*>(st) + ins * 256 + lane * 4) = f4{0.f, 0.f, 0.f, 0.f};
       }
-      __syncthreads();
+      lds_barrier();
     }
     if (kc + NS - 1 < nk) issue(kc + NS - 1, wrow, 0);
 #pragma unroll
@@ -464,7 +495,7 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd_kernel(MlpArgs a, float* __r
   } else {
     for (int kc = 0; kc < nk; ++kc) f1_chunk(kc);
   }
-  __syncthreads();  // staging is dead: Hs / W2s / Zs reuse it (PH 3: the momentum / X chunks of B1 start landing)
+  lds_barrier();  // staging is dead: Hs / W2s / Zs reuse it (PH 3: the momentum / X chunks of B1 start landing)
   // PH 3: B1's first NS - 1 chunks (momentum rows when UPD == 3, then X) fly during F2 .. B2
   if constexpr (PH == 3) {
     load_small();
@@ -491,8 +522,8 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd_kernel(MlpArgs a, float* __r
   }
   if constexpr (PH == 1) return;
   }  // PH != 2
-  for (int i = t; i < c * h; i += kThreads) W2s[(i / h) * hp + i % h] = wrow[oW2 + i];
-  __syncthreads();
+  lds_fill<8>(c * h, [&](int o) { return wrow[oW2 + o]; }, [&](int o, float v) { W2s[(o / h) * hp + o % h] = v; });
+  lds_barrier();
 
   DOL_TRACE(1)
   // ---- F2: Z2 = H W2^T + b2
@@ -509,7 +540,7 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd_kernel(MlpArgs a, float* __r
     }
     Zs[o] = ((s0 + s1) + (s2 + s3)) + b2s[j];
   }
-  __syncthreads();
+  lds_barrier();
 
   // ---- CE: log-softmax per sample, dZ2 = (p - onehot) / B
   if (t < B) {
@@ -525,7 +556,7 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd_kernel(MlpArgs a, float* __r
     const float invB = 1.0f / static_cast<float>(B);
     for (int j = 0; j < c; ++j) z[j] = (expf(z[j] - lse) - (j == y ? 1.0f : 0.0f)) * invB;
   }
-  __syncthreads();
+  lds_barrier();
   if (t == 0 && a.loss) {
     float s = 0.0f;
     for (int b = 0; b < B; ++b) s = s + ls[b];
@@ -568,6 +599,7 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd_kernel(MlpArgs a, float* __r
     if (o0 == 0) pw2.commit(a, wrow, grow, mrow, g, idx, ok);
     else pb.commit(a, wrow, grow, mrow, g, idx, ok);
   }
+  DOL_TRACE(5)
   if (t < 64) {  // db2 (c <= 32 lanes of wave 0)
     float g[1];
     const int j = t < c ? t : 0;
@@ -576,7 +608,8 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd_kernel(MlpArgs a, float* __r
     g[0] = s;
     pb2.commit(a, wrow, grow, mrow, g, idx_b2, ok_b2);
   }
-  __syncthreads();
+  lds_barrier();
+  DOL_TRACE(6)
 
   // ---- B2b: dZ1 = (dZ2 W2) * [H > 0], in place over H
   if (kThreads % h == 0 && B * h <= 16 * kThreads) {
@@ -612,7 +645,8 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd_kernel(MlpArgs a, float* __r
       *hv = (*hv > 0.0f) ? s : 0.0f;
     }
   }
-  __syncthreads();
+  lds_barrier();
+  DOL_TRACE(7)
 
   // ---- db1 (h <= kThreads)
   {
@@ -626,7 +660,7 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd_kernel(MlpArgs a, float* __r
 
   if constexpr (PH == 3) {
     DOL_TRACE(3)
-    __syncthreads();  // dZ1 complete in Hs
+    lds_barrier();  // dZ1 complete in Hs
     mlp_fused_dw1<UPD, NS, NK, KL>(a, wres, park, Hs, stg, rows, wrow, grow, mrow, issue, i0_b1, ipw);
     DOL_TRACE(4)
     return;
@@ -634,6 +668,84 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd_kernel(MlpArgs a, float* __r
   // dZ1 for the W1 tiles of mlp_dw1_kernel
   for (int o = t; o < B * h; o += kThreads) wsa[o] = Hs[(o / h) * hp + (o % h)];
   DOL_TRACE(3)
+}
+
+// F1 as one single-wave workgroup per (agent, 32-row h-tile), B <= 32 (r04):
+// H[:, 32 ht .. 32 ht + 32) = relu(W1[32 ht ..] X^T + b1) -> ws[agent][b][h],
+// then mlp_fwd_kernel PH 2 runs the per-agent tail from ws.  The per-agent F1
+// (4 waves, 61 KiB of staging, 2 workgroups per CU) streamed at 4.6 TB/s and
+// sat in lock step with the HBM-idle tail; here each wave owns its own
+// NS-deep LDS-DMA ring (W1 rows 0..31, X rows 32..63 of each 32-wide k chunk,
+// 16-B pieces swizzled by row as in mlp_fwd_kernel), no barriers, 8 KiB per
+// stage, so 4 - 5 independent rings share a CU.  X is fetched once per h-tile:
+// the nht tiles of an agent run on one XCD (blockIdx % 8 = agent % 8, tiles
+// consecutive), so the repeats meet in its L2.  Tail chunk pieces with k >= d
+// are out-of-range buffer lanes: they land as zeros, as mlp_fwd_kernel zeroes
+// them.  The MFMA sequence of a tile is the per-agent kernel's (same k order,
+// same operands): bit-identical H.
+template <int NS>
+__global__ __launch_bounds__(64) void mlp_f1_tile_kernel(MlpArgs a, float* __restrict__ ws, int n_agents) {
+  __shared__ __attribute__((aligned(16))) float stg[NS * 64 * 32];
+  const int B = a.B, d = a.d, h = a.h;
+  const int nht = h / 32;
+  const uint32_t bx = blockIdx.x, l = bx >> 3;
+  const int ht = static_cast<int>(l % uint32_t(nht));
+  const int agent = static_cast<int>((l / uint32_t(nht)) * 8 + (bx & 7));
+  if (agent >= n_agents) return;
+  const int lane = threadIdx.x;
+  const int li = lane & 31, hh = lane >> 5;
+  const float* wrow = a.W + int64_t(agent) * a.ldw;
+  const int64_t P1 = int64_t(h) * d + h + int64_t(a.c) * h + a.c;
+  const rsrc_t rsW = make_rsrc(wrow, P1 * 4);
+  const rsrc_t rsX = make_rsrc(a.X + int64_t(agent) * a.ldxa, (int64_t(B - 1) * a.ldxb + d) * 4);
+  const int nk = (d + 31) / 32;
+  // staged row r = 8 i + (lane >> 3): W1 row 32 ht + r (i < 4), X row min(r - 32, B - 1) (i >= 4)
+  const int ch = (lane & 7) ^ (lane >> 3);
+  uint32_t voff[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int r = 8 * i + (lane >> 3);
+    voff[i] = i < 4 ? uint32_t(((32 * ht + r) * d + 4 * ch) * 4) : uint32_t((min(r - 32, B - 1) * a.ldxb + 4 * ch) * 4);
+  }
+  auto issue = [&](int kc) {
+    float* st = stg + (kc % NS) * 64 * 32;
+    const bool pok = 32 * kc + 4 * ch < d;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(i < 4 ? rsW : rsX, DOL_LPTR(st + i * 256), 16,
+                                               static_cast<int>(pok ? voff[i] : kOOB), kc * 128, 0, 0);
+  };
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  for (int s0 = 0; s0 < NS - 1 && s0 < nk; ++s0) issue(s0);
+  for (int kc = 0; kc < nk; ++kc) {
+    wait_vmcnt(min(NS - 2, nk - 1 - kc) * 8);              // chunk kc landed (the next NS - 2 may still fly)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");    // last chunk's LDS reads done: its stage is free
+    if (kc + NS - 1 < nk) issue(kc + NS - 1);
+    const float* st = stg + (kc % NS) * 64 * 32;
+    const float* ar = st + li * 32;
+    const float* xr = st + (32 + li) * 32;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int pos = ((4 * hh + j) ^ (li & 7)) * 4;
+      const f4 av = *reinterpret_cast<const f4*>(ar + pos);
+      const f4 xv = *reinterpret_cast<const f4*>(xr + pos);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[q], xv[q], acc, 0, 0, 0);
+    }
+  }
+  // C/D map: col (b) = lane & 31, row (h) = (r&3) + 8*(r>>2) + 4*(lane>>5); bias + relu as mlp_fwd_kernel PH 1
+  if (li < B) {
+    float* wsa = ws + int64_t(agent) * B * h;
+    const int64_t ob1 = int64_t(h) * d;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int hr = 32 * ht + (r & 3) + 8 * (r >> 2) + 4 * hh;
+      const float z = acc[r] + wrow[ob1 + hr];
+      wsa[li * h + hr] = (z > 0.0f || z != z) ? z : 0.0f;
+    }
+  }
 }
 
 // B1 + W1 update: block agent * ndt + dt owns columns [32 dt, 32 dt + 32) of W1
@@ -791,6 +903,9 @@ extern "C" int dol_mlp_step_f32(float* w, int64_t ldw, float* grad, int64_t ldg,
   // DOL_MLP_SPLIT_FWD=1: measured 0.518-0.524 (F1 depth 3 / 4) and 0.509-0.511
   // (depth 2) vs 0.509-0.513 ms fused (profiles/r03_mlp_split_fwd.txt)
   static const int split_fwd = [] { const char* e = getenv("DOL_MLP_SPLIT_FWD"); return e ? atoi(e) : 0; }();
+  // F1 as single-wave (agent, h-tile) workgroups with NS-deep rings (mlp_f1_tile_kernel;
+  // DOL_MLP_F1_TILES = NS in {3, 4, 5, 6, 8}, 0 = off), B <= 32
+  static const int f1_tile_ns = [] { const char* e = getenv("DOL_MLP_F1_TILES"); return e ? atoi(e) : 0; }();
   const int upd = update ? mode + 1 : 0;
   float* ws = static_cast<float*>(work);
   // dW1 tile order (DOL_MLP_DW1_XCD: 1 = an agent's tiles on one XCD, 0 = agent-major)
@@ -841,7 +956,20 @@ extern "C" int dol_mlp_step_f32(float* w, int64_t ldw, float* grad, int64_t ldg,
         return;
       }
     }
-    if (split_fwd) {  // F1 kernel (staging only in LDS), then the per-agent tail kernel
+    // the per-agent tail (PH 2) needs no F1 staging: LDS = its post-F1 arrays alone
+    auto tail = [&] {
+      if (nt1) fwd(mlp_fwd_kernel<1, U, TH, AL, 1, 2>, lds_for(1));
+      else fwd(mlp_fwd_kernel<4, U, TH, AL, 1, 2>, lds_for(1));
+    };
+    if (f1_tile_ns && B <= 32 && P * 4 < (int64_t(1) << 31)) {  // F1 per (agent, h-tile), then the tail
+      const dim3 gt(static_cast<unsigned>(int64_t(h / 32) * ((int64_t(n_agents) + 7) / 8 * 8))), bt(64);
+      if (f1_tile_ns == 3) hipLaunchKernelGGL(mlp_f1_tile_kernel<3>, gt, bt, 0, s, a, ws, n_agents);
+      else if (f1_tile_ns == 4) hipLaunchKernelGGL(mlp_f1_tile_kernel<4>, gt, bt, 0, s, a, ws, n_agents);
+      else if (f1_tile_ns == 6) hipLaunchKernelGGL(mlp_f1_tile_kernel<6>, gt, bt, 0, s, a, ws, n_agents);
+      else if (f1_tile_ns == 8) hipLaunchKernelGGL(mlp_f1_tile_kernel<8>, gt, bt, 0, s, a, ws, n_agents);
+      else hipLaunchKernelGGL(mlp_f1_tile_kernel<5>, gt, bt, 0, s, a, ws, n_agents);
+      tail();
+    } else if (split_fwd) {  // F1 kernel (staging only in LDS), then the per-agent tail kernel
       auto f1 = [&](auto ns_c) {
         constexpr int NS = decltype(ns_c)::value;
         const size_t l1 = sizeof(float) * size_t(NS) * (h + 32 * ((B + 31) / 32)) * 32;
@@ -852,8 +980,7 @@ extern "C" int dol_mlp_step_f32(float* w, int64_t ldw, float* grad, int64_t ldg,
       else if (stages == 4) f1(std::integral_constant<int, 4>{});
       else if (stages == 5) f1(std::integral_constant<int, 5>{});
       else f1(std::integral_constant<int, 3>{});
-      if (nt1) fwd(mlp_fwd_kernel<1, U, TH, AL, kStages, 2>, lds);
-      else fwd(mlp_fwd_kernel<4, U, TH, AL, kStages, 2>, lds);
+      tail();
     } else if (stages == 2) {
       if (nt1) fwd(mlp_fwd_kernel<1, U, TH, AL, 2>, lds_for(2));
       else fwd(mlp_fwd_kernel<4, U, TH, AL, 2>, lds_for(2));

@@ -91,15 +91,17 @@ MAPPED_MIN_BYTES = 1 << 30
 
 
 def device_matrix(rows: int, cols: int, device, zero: bool = False) -> torch.Tensor:
-    """A [rows, cols] fp32 device matrix for bank state.  Large ones (>= 1 GiB)
-    are ONE mapped physical allocation (dol_bank_alloc: hipMemCreate +
-    hipMemMap) instead of a caching-allocator block: the ring round at 8192 x
-    2^20 ran 10.93-10.96 ms on such buffers against 11.15-11.17 on hipMalloc'd
-    ones, alternating in one process (tools/alloc_probe.hip,
-    profiles/r04e_alloc_probe.jsonl).  DOL_BANK_ALLOC=torch keeps torch's
-    allocator for everything."""
+    """A [rows, cols] fp32 device matrix for bank state, from torch's caching
+    allocator.  DOL_BANK_ALLOC=vmm (opt-in) makes large ones (>= 1 GiB) ONE
+    mapped physical allocation (dol_bank_alloc: hipMemCreate + hipMemMap): the
+    ring round at 8192 x 2^20 ran 10.93-10.96 ms on such buffers against
+    11.15-11.17 on hipMalloc'd ones, alternating in one process
+    (tools/alloc_probe.hip, profiles/r04e_alloc_probe.jsonl).  Not the
+    default: a process that mapped, freed and re-mapped eleven 4 GiB blocks in
+    a row (tools/bench_configs.py's DGD rounds) once ended in a GPU memory
+    fault (r04, profiles/r04k_vmm_fault.txt), cause not isolated."""
     device = torch.device(device)
-    if (os.environ.get("DOL_BANK_ALLOC", "vmm") == "vmm" and device.type == "cuda"
+    if (os.environ.get("DOL_BANK_ALLOC", "torch") == "vmm" and device.type == "cuda"
             and rows * cols * 4 >= MAPPED_MIN_BYTES):
         t = torch.as_tensor(_MappedBlock(rows, cols, device), device=device)
         if zero:

@@ -41,7 +41,7 @@ def test_mapped_matrix_round_trip_and_mix(gpu, monkeypatch):
     torch.cuda.synchronize()
 
 
-def test_bank_uses_mapped_buffers_for_large_state(gpu, monkeypatch):
+def test_bank_maps_large_state_when_asked(gpu, monkeypatch):
     made = []
 
     class Spy(B._MappedBlock):
@@ -52,6 +52,9 @@ def test_bank_uses_mapped_buffers_for_large_state(gpu, monkeypatch):
     monkeypatch.setattr(B, "_MappedBlock", Spy)
     monkeypatch.setattr(B, "MAPPED_MIN_BYTES", 1 << 20)
     monkeypatch.delenv("DOL_BANK_ALLOC", raising=False)
+    B.AgentBank(64, 8192, gpu).buffer("x")  # default: torch's allocator
+    assert made == []
+    monkeypatch.setenv("DOL_BANK_ALLOC", "vmm")
     bank = B.AgentBank(64, 8192, gpu)  # 2 MiB per buffer: mapped
     x = bank.buffer("x", zero=True)
     assert made == [x.data_ptr()] and float(x.abs().sum()) == 0.0

@@ -58,6 +58,9 @@ def test_argument_errors_are_reported_without_launch():
     assert rc == -1 and b"alias" in L.dol_last_error()
     rc = L.dol_mix_dense_split3_f32(fake, 8, fake + 4096, 8, fake + 8192, 8, 8, 8, 8, fake, 16, 0, None)
     assert rc == -1 and b"workspace" in L.dol_last_error()
+    # only blocks dol_bank_alloc handed out are unmapped (checked before any HIP call)
+    assert L.dol_bank_free(fake, 1 << 21) == -1 and b"not a dol_bank_alloc block" in L.dol_last_error()
+    assert L.dol_bank_free(None, 1 << 21) == 0
 
 
 def test_pm_stage_order_setter():

@@ -82,6 +82,43 @@ int main(int argc, char** argv) {
     for (int p = 0; p < 4; ++p) printf("  %-20s %8.1f us\n", names[p], sum[p] / n / 100.0);
     return 0;
   }
+  if (argc > 2 && argv[2][0] == 't') {  // F1 tiles + the per-agent tail (PH 2): phases load, F2+CE, B2
+    const size_t lt = sizeof(float) * (fwd_union_floats(B, h, c, 1) + h + c + B) + 4 * B;
+    auto k = mlp_fwd_kernel<1, 3, false, false, 1, 2>;
+    const dim3 gt(unsigned(h / 32 * ((n + 7) / 8 * 8)));
+    for (int it = 0; it < 3; ++it) {
+      hipLaunchKernelGGL(mlp_f1_tile_kernel<5>, gt, dim3(64), 0, 0, a, ws, n);
+      hipLaunchKernelGGL(k, dim3(n), dim3(kThreads), lt, 0, a, ws);
+    }
+    hipLaunchKernelGGL(mlp_f1_tile_kernel<5>, gt, dim3(64), 0, 0, a, ws, n);
+    CHECK(hipEventRecord(e0));
+    hipLaunchKernelGGL(k, dim3(n), dim3(kThreads), lt, 0, a, ws);
+    CHECK(hipEventRecord(e1));
+    CHECK(hipEventSynchronize(e1));
+    float ms;
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    std::vector<long long> ht(int64_t(n) * 8);
+    CHECK(hipMemcpy(ht.data(), tr, ht.size() * 8, hipMemcpyDeviceToHost));
+    // stamps: 0 start, 1 H + W2 in LDS, 2 after CE, 5 after dW2 (+ its stores issued), 6 after db2 +
+    // barrier, 7 after dZ1 + barrier, 3 end (db1, dZ1 -> ws)
+    const char* names[] = {"load H, W2", "F2+CE", "B2a dW2", "db2+barrier", "B2b dZ1", "db1+dZ1 out"};
+    const int from[] = {0, 1, 2, 5, 6, 7}, to[] = {1, 2, 5, 6, 7, 3};
+    double sum[6] = {0, 0, 0, 0, 0, 0};
+    long long t0 = ht[0], tend = ht[3];
+    for (int i = 0; i < n; ++i) {
+      t0 = std::min(t0, ht[i * 8]);
+      tend = std::max(tend, ht[i * 8 + 3]);
+      for (int p = 0; p < 6; ++p) sum[p] += double(ht[i * 8 + to[p]] - ht[i * 8 + from[p]]);
+    }
+    printf("tail kernel %.3f ms (%d agents), span(stamps) %.3f ms\n", ms, n, (tend - t0) / 1e5);
+    for (int p = 0; p < 6; ++p) printf("  %-20s %8.1f us\n", names[p], sum[p] / n / 100.0);
+    int hist[10] = {0};
+    for (int i = 0; i < n; ++i) hist[std::min(int(10.0 * (ht[i * 8] - t0) / double(tend - t0 + 1)), 9)]++;
+    printf("  WG starts per 10%% of span:");
+    for (int b = 0; b < 10; ++b) printf(" %d", hist[b]);
+    printf("\n");
+    return 0;
+  }
   for (int it = 0; it < 3; ++it) {
     hipLaunchKernelGGL((mlp_fwd_kernel<1, 3, false, false>), dim3(n), dim3(kThreads), lds, 0, a, ws);
     hipLaunchKernelGGL((mlp_dw1_kernel<16, 3, false, false>), g2, dim3(kThreads), 0, 0, a, ws, n);
