@@ -190,6 +190,28 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
+// two arrays in one round trip when each fits one batch
+template <int N1, int N2, class S1, class D1, class S2, class D2>
+__device__ __forceinline__ void lds_fill2(int n1, S1 src1, D1 dst1, int n2, S2 src2, D2 dst2) {
+  if (n1 > N1 * kThreads || n2 > N2 * kThreads) {
+    lds_fill<N1>(n1, src1, dst1);
+    lds_fill<N2>(n2, src2, dst2);
+    return;
+  }
+  const int t = threadIdx.x;
+  float v1[N1], v2[N2];
+#pragma unroll
+  for (int i = 0; i < N1; ++i) v1[i] = src1(i * kThreads + t < n1 ? i * kThreads + t : 0);
+#pragma unroll
+  for (int i = 0; i < N2; ++i) v2[i] = src2(i * kThreads + t < n2 ? i * kThreads + t : 0);
+#pragma unroll
+  for (int i = 0; i < N1; ++i)
+    if (i * kThreads + t < n1) dst1(i * kThreads + t, v1[i]);
+#pragma unroll
+  for (int i = 0; i < N2; ++i)
+    if (i * kThreads + t < n2) dst2(i * kThreads + t, v2[i]);
+}
+
 constexpr int kStages = 3;  // default F1 LDS-DMA pipeline depth (NS - 1 chunks in flight during the MFMAs)
 
 // LDS layout of mlp_fwd_kernel (floats): [ union: F1 staging | Hs, W2s, Zs ] [ b1s, b2s, ls ] [ ys ];
@@ -392,6 +414,8 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd_kernel(MlpArgs a, float* __r
     for (int i = t; i < h; i += kThreads) b1s[i] = wrow[ob1 + i];
   if constexpr (PH != 1) lds_barrier();  // PH 1: the staging is the whole LDS (b1 read from memory below)
   float* wsa = ws + int64_t(agent) * B * h;  // H (PH 1 -> 2), then dZ1 for mlp_dw1_kernel
+  // pw2 holds W2 itself when the update (or the prox term) loaded it and it fits one batch
+  const bool w2_in_regs = (UPD > 0 || TH) && c * h <= 8 * kThreads;
   // ---- F1: Z1^T tiles (32 h x 32 b) on MFMA, K = d in chunks of 32
   const int nht = h / 32, nbt = (B + 31) / 32;
   const int Bp = 32 * nbt, rows = PH == 3 ? 160 : h + Bp;  // staged rows per chunk (W1 rows, then X rows)
@@ -445,7 +469,11 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd_kernel(MlpArgs a, float* __r
   f4 wres[PH == 3 ? NK - KL : 1][4];
   const int i0_b1 = UPD == 3 ? 0 : PH == 3 ? 4 : h / 32;  // PH 3's B1 chunks: momentum rows (UPD 3) + X rows, or X rows only
   if constexpr (PH == 2) {  // H from the F1 kernel
-    lds_fill<16>(B * h, [&](int o) { return wsa[o]; }, [&](int o, float v) { Hs[(o / h) * hp + (o % h)] = v; });
+    if (w2_in_regs)
+      lds_fill<16>(B * h, [&](int o) { return wsa[o]; }, [&](int o, float v) { Hs[(o / h) * hp + (o % h)] = v; });
+    else
+      lds_fill2<16, 8>(B * h, [&](int o) { return wsa[o]; }, [&](int o, float v) { Hs[(o / h) * hp + (o % h)] = v; },
+                       c * h, [&](int o) { return wrow[oW2 + o]; }, [&](int o, float v) { W2s[(o / h) * hp + o % h] = v; });
   } else {
 
   f32x16 acc[NT];
@@ -522,7 +550,13 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd_kernel(MlpArgs a, float* __r
   }
   if constexpr (PH == 1) return;
   }  // PH != 2
-  lds_fill<8>(c * h, [&](int o) { return wrow[oW2 + o]; }, [&](int o, float v) { W2s[(o / h) * hp + o % h] = v; });
+  if (w2_in_regs) {  // W2 from the update operands loaded at the start: no memory round trip here
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if (ok_w2(i)) W2s[((i * kThreads + t) / h) * hp + (i * kThreads + t) % h] = pw2.w[i];
+  } else if constexpr (PH != 2) {  // (PH 2 filled W2s together with H)
+    lds_fill<8>(c * h, [&](int o) { return wrow[oW2 + o]; }, [&](int o, float v) { W2s[(o / h) * hp + o % h] = v; });
+  }
   lds_barrier();
 
   DOL_TRACE(1)
@@ -530,6 +564,7 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd_kernel(MlpArgs a, float* __r
   for (int o = t; o < B * c; o += kThreads) {
     const int b = o / c, j = o % c;
     float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;  // h % 32 == 0
+#pragma unroll 8
     for (int k = 0; k < h; k += 4) {
       const f4 hv = *reinterpret_cast<const f4*>(Hs + b * hp + k);
       const f4 wv = *reinterpret_cast<const f4*>(W2s + j * hp + k);
@@ -559,6 +594,7 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd_kernel(MlpArgs a, float* __r
   lds_barrier();
   if (t == 0 && a.loss) {
     float s = 0.0f;
+#pragma unroll 8
     for (int b = 0; b < B; ++b) s = s + ls[b];
     a.loss[agent] = s / static_cast<float>(B);
   }
@@ -580,6 +616,7 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd_kernel(MlpArgs a, float* __r
         jj[i] = ok(i) ? (o0 + i * kThreads + t) / h : 0;
         g[i] = 0.0f;
       }
+#pragma unroll 4
       for (int b = 0; b < B; ++b) {  // per output the same products, summed over b ascending
         const float hv = Hs[b * hp + k];
         const float* zr = Zs + b * c;
@@ -604,6 +641,7 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd_kernel(MlpArgs a, float* __r
     float g[1];
     const int j = t < c ? t : 0;
     float s = 0.0f;
+#pragma unroll 8
     for (int b = 0; b < B; ++b) s = s + Zs[b * c + j];
     g[0] = s;
     pb2.commit(a, wrow, grow, mrow, g, idx_b2, ok_b2);
@@ -624,7 +662,9 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd_kernel(MlpArgs a, float* __r
 #pragma unroll
       for (int m = 0; m < 16; ++m) {
         const int b = b0 + m * bs;
-        if (b < B) sm[m] = sm[m] + Zs[b * c + j] * w2;
+        // unconditional read (b clamped; rows b >= B are never stored): a branch per
+        // sample serialised the 16 reads, one LDS round trip each (8.5 us per agent)
+        sm[m] = sm[m] + Zs[min(b, B - 1) * c + j] * w2;
       }
     }
 #pragma unroll
@@ -653,6 +693,7 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd_kernel(MlpArgs a, float* __r
     float g[1];
     float s = 0.0f;
     if (t < h)
+#pragma unroll 8
       for (int b = 0; b < B; ++b) s = s + Hs[b * hp + t];
     g[0] = s;
     pb1.commit(a, wrow, grow, mrow, g, idx_b1, ok_b1);
