@@ -90,7 +90,7 @@ class _MappedBlock:
 MAPPED_MIN_BYTES = 1 << 30
 
 
-def device_matrix(rows: int, cols: int, device, zero: bool = False) -> torch.Tensor:
+def device_matrix(rows: int, cols: int, device, zero: bool = False, mapped: Optional[bool] = None) -> torch.Tensor:
     """A [rows, cols] fp32 device matrix for bank state, from torch's caching
     allocator.  DOL_BANK_ALLOC=vmm (opt-in) makes large ones (>= 1 GiB) ONE
     mapped physical allocation (dol_bank_alloc: hipMemCreate + hipMemMap): the
@@ -99,10 +99,12 @@ def device_matrix(rows: int, cols: int, device, zero: bool = False) -> torch.Ten
     (tools/alloc_probe.hip, profiles/r04e_alloc_probe.jsonl).  Not the
     default: a process that mapped, freed and re-mapped eleven 4 GiB blocks in
     a row (tools/bench_configs.py's DGD rounds) once ended in a GPU memory
-    fault (r04, profiles/r04k_vmm_fault.txt), cause not isolated."""
+    fault (r04, profiles/r04k_vmm_fault.txt), cause not isolated.  mapped=True
+    / False decides for this matrix regardless of the environment (bench.py
+    maps the headline ring's two buffers, allocated once per process)."""
     device = torch.device(device)
-    if (os.environ.get("DOL_BANK_ALLOC", "torch") == "vmm" and device.type == "cuda"
-            and rows * cols * 4 >= MAPPED_MIN_BYTES):
+    want = os.environ.get("DOL_BANK_ALLOC", "torch") == "vmm" if mapped is None else bool(mapped)
+    if want and device.type == "cuda" and rows * cols * 4 >= MAPPED_MIN_BYTES:
         t = torch.as_tensor(_MappedBlock(rows, cols, device), device=device)
         if zero:
             t.zero_()

@@ -91,12 +91,14 @@ def shard_bounds(n: int, world: int, rank: int) -> Tuple[int, int]:
 class ShardedRing:
     """Ring (circle) mixing of a globally N-agent system, sharded by rows.
 
-    x/y: local [n_local, ld] buffers (allocated here); w_prev/w_next: the
-    GLOBAL ring weights [N] (host or device); the local slice is kept.
+    x/y: local [n_local, ld] buffers (allocated here; mapped as
+    bank.device_matrix); w_prev/w_next: the GLOBAL ring weights [N] (host or
+    device); the local slice is kept.
     """
 
     def __init__(self, n_agents: int, P: int, w_prev, w_next, device, ld: Optional[int] = None,
-                 group=None, alloc: bool = True, mix_ring=None, dgd_ring=None, mix_edges=None, dgd_edges=None):
+                 group=None, alloc: bool = True, mix_ring=None, dgd_ring=None, mix_edges=None, dgd_edges=None,
+                 mapped: Optional[bool] = None):
         # mix_ring / dgd_ring / *_edges: kernel entries (default: the HIP ops); tests
         # inject CPU checkers.  The boundary rows go in ONE launch (dol_*_ring_edges_f32);
         # with an injected mix and no injected edge entry they go through the mix, one row each.
@@ -121,8 +123,8 @@ class ShardedRing:
         self.prev_rank = (self.rank - 1) % self.world
         self.next_rank = (self.rank + 1) % self.world
         if alloc:
-            self.x = device_matrix(self.n_local, self.ld, self.device)
-            self.y = device_matrix(self.n_local, self.ld, self.device)
+            self.x = device_matrix(self.n_local, self.ld, self.device, mapped=mapped)
+            self.y = device_matrix(self.n_local, self.ld, self.device, mapped=mapped)
         self.halo_prev = torch.empty(self.ld, dtype=torch.float32, device=self.device)
         self.halo_next = torch.empty(self.ld, dtype=torch.float32, device=self.device)
         # optional (start, end) timing events recorded around the interior kernel
