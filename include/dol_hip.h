@@ -452,9 +452,12 @@ int dol_er_stochastic_f32(float* W, int64_t ldw, int32_t n, float p, uint64_t se
  * Device memory for a bank buffer as ONE physical allocation (hipMemCreate)
  * mapped into a reserved virtual range (hipMemAddressReserve + hipMemMap),
  * rounded up to the allocation granularity (*mapped_bytes).  Free with
- * dol_bank_free(ptr, *mapped_bytes).  Host-side, synchronous, not
- * graph-capturable.  No reference counterpart (the reference keeps one
- * nn.Module per agent in host memory).
+ * dol_bank_free(ptr, *mapped_bytes), which unmaps the range and then
+ * releases the physical allocation; it refuses a pointer this library did not
+ * hand out (DOL_EINVAL, before any HIP call) and accepts NULL.  Host-side,
+ * synchronous, thread-safe, not graph-capturable.  Opt-in for bank buffers
+ * (bank.device_matrix, DOL_BANK_ALLOC=vmm).  No reference counterpart (the
+ * reference keeps one nn.Module per agent in host memory).
  */
 int dol_bank_alloc(int64_t bytes, void** ptr, int64_t* mapped_bytes);
 int dol_bank_free(void* ptr, int64_t mapped_bytes);
