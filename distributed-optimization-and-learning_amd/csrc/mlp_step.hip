@@ -363,7 +363,7 @@ __device__ __forceinline__ void mlp_fused_dw1(const MlpArgs& a, const f4 (&wres)
 // (tests/test_mlp_gpu.py::test_step_paths_bit_identical), opt-in
 // (DOL_MLP_FUSED=1): see the measurement at the dispatch below.
 template <int NT, int UPD, bool TH, bool AL, int NS = kStages, int PH = 0, int NK = 0>
-__global__ __launch_bounds__(kThreads) void mlp_fwd_kernel(MlpArgs a, float* __restrict__ ws) {
+__device__ __forceinline__ void mlp_fwd_body(MlpArgs a, float* __restrict__ ws) {
   static_assert(PH != 3 || (NT == 1 && NK > 0 && !TH && !AL && UPD >= 1), "fused step: plain / momentum SGD, one tile per wave");
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int B = a.B, d = a.d, h = a.h, c = a.c;
@@ -711,6 +711,20 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd_kernel(MlpArgs a, float* __r
   DOL_TRACE(3)
 }
 
+template <int NT, int UPD, bool TH, bool AL, int NS = kStages, int PH = 0, int NK = 0>
+__global__ __launch_bounds__(kThreads) void mlp_fwd_kernel(MlpArgs a, float* __restrict__ ws) {
+  mlp_fwd_body<NT, UPD, TH, AL, NS, PH, NK>(a, ws);
+}
+
+// the per-agent tail (PH 2) compiled for four waves per SIMD (<= 128 VGPRs,
+// r04): at the default three (151 VGPRs) 1024 agents ran as two rounds of
+// 768 + 256 workgroups (tools/mlp_phase.hip 't')
+template <int NT, int UPD, bool TH, bool AL>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void mlp_tail_kernel(
+    MlpArgs a, float* __restrict__ ws) {
+  mlp_fwd_body<NT, UPD, TH, AL, 1, 2, 0>(a, ws);
+}
+
 // F1 as one single-wave workgroup per (agent, 32-row h-tile), B <= 32 (r04):
 // H[:, 32 ht .. 32 ht + 32) = relu(W1[32 ht ..] X^T + b1) -> ws[agent][b][h],
 // then mlp_fwd_kernel PH 2 runs the per-agent tail from ws.  The per-agent F1
@@ -724,9 +738,17 @@ __global__ __launch_bounds__(kThreads) void mlp_fwd_kernel(MlpArgs a, float* __r
 // are out-of-range buffer lanes: they land as zeros, as mlp_fwd_kernel zeroes
 // them.  The MFMA sequence of a tile is the per-agent kernel's (same k order,
 // same operands): bit-identical H.
-template <int NS>
+// KW (k chunk width): 32 = 128-B row pieces, 8 rows per DMA instruction; 64 =
+// 256-B pieces, 4 rows per instruction, each 64-wide chunk consumed as two
+// 32-wide halves in k order (a half wholly past d is skipped, as the 32-wide
+// kernel never stages it): the same MFMA sequence either way.
+template <int NS, int KW = 32>
 __global__ __launch_bounds__(64) void mlp_f1_tile_kernel(MlpArgs a, float* __restrict__ ws, int n_agents) {
-  __shared__ __attribute__((aligned(16))) float stg[NS * 64 * 32];
+  static_assert(KW == 32 || KW == 64, "k chunk: 32 or 64 floats");
+  constexpr int PPR = KW / 4;     // 16-B pieces per staged row (slot = piece ^ (row % PPR))
+  constexpr int RPI = 64 / PPR;   // staged rows per DMA instruction
+  constexpr int NI = 64 / RPI;    // DMA instructions per stage (64 staged rows)
+  __shared__ __attribute__((aligned(16))) float stg[NS * 64 * KW];
   const int B = a.B, d = a.d, h = a.h;
   const int nht = h / 32;
   const uint32_t bx = blockIdx.x, l = bx >> 3;
@@ -739,41 +761,47 @@ __global__ __launch_bounds__(64) void mlp_f1_tile_kernel(MlpArgs a, float* __res
   const int64_t P1 = int64_t(h) * d + h + int64_t(a.c) * h + a.c;
   const rsrc_t rsW = make_rsrc(wrow, P1 * 4);
   const rsrc_t rsX = make_rsrc(a.X + int64_t(agent) * a.ldxa, (int64_t(B - 1) * a.ldxb + d) * 4);
-  const int nk = (d + 31) / 32;
-  // staged row r = 8 i + (lane >> 3): W1 row 32 ht + r (i < 4), X row min(r - 32, B - 1) (i >= 4)
-  const int ch = (lane & 7) ^ (lane >> 3);
-  uint32_t voff[8];
+  const int nk = (d + KW - 1) / KW;
+  // staged row r = RPI i + lane / PPR: W1 row 32 ht + r (r < 32), X row min(r - 32, B - 1) (r >= 32);
+  // lane's LDS slot lane % PPR holds piece slot ^ (r % PPR)
+  uint32_t voff[NI];
+  int pc[NI];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int r = 8 * i + (lane >> 3);
-    voff[i] = i < 4 ? uint32_t(((32 * ht + r) * d + 4 * ch) * 4) : uint32_t((min(r - 32, B - 1) * a.ldxb + 4 * ch) * 4);
+  for (int i = 0; i < NI; ++i) {
+    const int r = RPI * i + lane / PPR;
+    pc[i] = (lane % PPR) ^ (r % PPR);
+    voff[i] = r < 32 ? uint32_t(((32 * ht + r) * d + 4 * pc[i]) * 4) : uint32_t((min(r - 32, B - 1) * a.ldxb + 4 * pc[i]) * 4);
   }
   auto issue = [&](int kc) {
-    float* st = stg + (kc % NS) * 64 * 32;
-    const bool pok = 32 * kc + 4 * ch < d;
+    float* st = stg + (kc % NS) * 64 * KW;
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(i < 4 ? rsW : rsX, DOL_LPTR(st + i * 256), 16,
-                                               static_cast<int>(pok ? voff[i] : kOOB), kc * 128, 0, 0);
+    for (int i = 0; i < NI; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(RPI * i < 32 ? rsW : rsX, DOL_LPTR(st + i * 256), 16,
+                                               static_cast<int>(KW * kc + 4 * pc[i] < d ? voff[i] : kOOB), kc * KW * 4,
+                                               0, 0);
   };
   f32x16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
   for (int s0 = 0; s0 < NS - 1 && s0 < nk; ++s0) issue(s0);
   for (int kc = 0; kc < nk; ++kc) {
-    wait_vmcnt(min(NS - 2, nk - 1 - kc) * 8);              // chunk kc landed (the next NS - 2 may still fly)
+    wait_vmcnt(min(NS - 2, nk - 1 - kc) * NI);             // chunk kc landed (the next NS - 2 may still fly)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");    // last chunk's LDS reads done: its stage is free
     if (kc + NS - 1 < nk) issue(kc + NS - 1);
-    const float* st = stg + (kc % NS) * 64 * 32;
-    const float* ar = st + li * 32;
-    const float* xr = st + (32 + li) * 32;
+    const float* st = stg + (kc % NS) * 64 * KW;
+    const float* ar = st + li * KW;
+    const float* xr = st + (32 + li) * KW;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int pos = ((4 * hh + j) ^ (li & 7)) * 4;
-      const f4 av = *reinterpret_cast<const f4*>(ar + pos);
-      const f4 xv = *reinterpret_cast<const f4*>(xr + pos);
+    for (int h2 = 0; h2 < KW / 32; ++h2) {
+      if (h2 > 0 && KW * kc + 32 * h2 >= d) break;  // a half wholly past d (wave-uniform)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[q], xv[q], acc, 0, 0, 0);
+      for (int j = 0; j < 4; ++j) {
+        const int pos = ((8 * h2 + 4 * hh + j) ^ (li % PPR)) * 4;
+        const f4 av = *reinterpret_cast<const f4*>(ar + pos);
+        const f4 xv = *reinterpret_cast<const f4*>(xr + pos);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[q], xv[q], acc, 0, 0, 0);
+      }
     }
   }
   // C/D map: col (b) = lane & 31, row (h) = (r&3) + 8*(r>>2) + 4*(lane>>5); bias + relu as mlp_fwd_kernel PH 1
@@ -947,6 +975,10 @@ extern "C" int dol_mlp_step_f32(float* w, int64_t ldw, float* grad, int64_t ldg,
   // F1 as single-wave (agent, h-tile) workgroups with NS-deep rings (mlp_f1_tile_kernel;
   // DOL_MLP_F1_TILES = NS in {3, 4, 5, 6, 8}, 0 = off), B <= 32
   static const int f1_tile_ns = [] { const char* e = getenv("DOL_MLP_F1_TILES"); return e ? atoi(e) : 0; }();
+  // its k chunk width (DOL_MLP_F1_KW = 32 / 64; 64 takes NS 3 or 4) and the
+  // tail's occupancy (DOL_MLP_TAIL_OCC = 4: mlp_tail_kernel, <= 128 VGPRs)
+  static const int f1_kw = [] { const char* e = getenv("DOL_MLP_F1_KW"); return e ? atoi(e) : 32; }();
+  static const int tail_occ4 = [] { const char* e = getenv("DOL_MLP_TAIL_OCC"); return e ? atoi(e) == 4 : 0; }();
   const int upd = update ? mode + 1 : 0;
   float* ws = static_cast<float*>(work);
   // dW1 tile order (DOL_MLP_DW1_XCD: 1 = an agent's tiles on one XCD, 0 = agent-major)
@@ -999,12 +1031,21 @@ extern "C" int dol_mlp_step_f32(float* w, int64_t ldw, float* grad, int64_t ldg,
     }
     // the per-agent tail (PH 2) needs no F1 staging: LDS = its post-F1 arrays alone
     auto tail = [&] {
-      if (nt1) fwd(mlp_fwd_kernel<1, U, TH, AL, 1, 2>, lds_for(1));
-      else fwd(mlp_fwd_kernel<4, U, TH, AL, 1, 2>, lds_for(1));
+      if (tail_occ4) {
+        if (nt1) fwd(mlp_tail_kernel<1, U, TH, AL>, lds_for(1));
+        else fwd(mlp_tail_kernel<4, U, TH, AL>, lds_for(1));
+      } else if (nt1) {
+        fwd(mlp_fwd_kernel<1, U, TH, AL, 1, 2>, lds_for(1));
+      } else {
+        fwd(mlp_fwd_kernel<4, U, TH, AL, 1, 2>, lds_for(1));
+      }
     };
     if (f1_tile_ns && B <= 32 && P * 4 < (int64_t(1) << 31)) {  // F1 per (agent, h-tile), then the tail
       const dim3 gt(static_cast<unsigned>(int64_t(h / 32) * ((int64_t(n_agents) + 7) / 8 * 8))), bt(64);
-      if (f1_tile_ns == 3) hipLaunchKernelGGL(mlp_f1_tile_kernel<3>, gt, bt, 0, s, a, ws, n_agents);
+      if (f1_kw == 64) {
+        if (f1_tile_ns == 4) hipLaunchKernelGGL((mlp_f1_tile_kernel<4, 64>), gt, bt, 0, s, a, ws, n_agents);
+        else hipLaunchKernelGGL((mlp_f1_tile_kernel<3, 64>), gt, bt, 0, s, a, ws, n_agents);
+      } else if (f1_tile_ns == 3) hipLaunchKernelGGL(mlp_f1_tile_kernel<3>, gt, bt, 0, s, a, ws, n_agents);
       else if (f1_tile_ns == 4) hipLaunchKernelGGL(mlp_f1_tile_kernel<4>, gt, bt, 0, s, a, ws, n_agents);
       else if (f1_tile_ns == 6) hipLaunchKernelGGL(mlp_f1_tile_kernel<6>, gt, bt, 0, s, a, ws, n_agents);
       else if (f1_tile_ns == 8) hipLaunchKernelGGL(mlp_f1_tile_kernel<8>, gt, bt, 0, s, a, ws, n_agents);

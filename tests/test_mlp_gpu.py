@@ -189,11 +189,14 @@ print("ok")
 
 
 _STEP_PATHS = {  # env of each alternative launch path (read once per process: run in children)
-    "base": dict(DOL_MLP_FUSED="0", DOL_MLP_SPLIT_FWD="0", DOL_MLP_F1_TILES="0"),
+    "base": dict(DOL_MLP_FUSED="0", DOL_MLP_SPLIT_FWD="0", DOL_MLP_F1_TILES="0", DOL_MLP_F1_KW="32", DOL_MLP_TAIL_OCC="3"),
     "fused": dict(DOL_MLP_FUSED="1"),
     "split": dict(DOL_MLP_SPLIT_FWD="1"),
     "f1tiles4": dict(DOL_MLP_F1_TILES="4"),
     "f1tiles5": dict(DOL_MLP_F1_TILES="5"),
+    "f1tiles3kw64": dict(DOL_MLP_F1_TILES="3", DOL_MLP_F1_KW="64", DOL_MLP_TAIL_OCC="4"),
+    "f1tiles4kw64": dict(DOL_MLP_F1_TILES="4", DOL_MLP_F1_KW="64"),
+    "split_tail4": dict(DOL_MLP_SPLIT_FWD="1", DOL_MLP_TAIL_OCC="4"),
 }
 
 
@@ -211,14 +214,15 @@ def _run_step_child(root, tmp_path, name):
     return torch.load(f, weights_only=True)
 
 
-@pytest.mark.parametrize("path", ["fused", "split", "f1tiles4", "f1tiles5"])
+@pytest.mark.parametrize("path", ["fused", "split", "f1tiles4", "f1tiles5", "f1tiles3kw64", "f1tiles4kw64", "split_tail4"])
 def test_step_paths_bit_identical(path, gpu, tmp_path):
     """Each alternative launch path of the step gives the same parameters,
     momentum, gradients and losses as the default forward + dW1 kernels, bit
     for bit: the one-kernel step with W1 resident in registers
     (DOL_MLP_FUSED=1), F1 as its own per-agent kernel (DOL_MLP_SPLIT_FWD=1)
-    and F1 per (agent, h-tile) single-wave workgroups (DOL_MLP_F1_TILES=NS),
-    each followed by the per-agent tail.  Cases: d with and without a partial
+    and F1 per (agent, h-tile) single-wave workgroups (DOL_MLP_F1_TILES=NS,
+    32- or 64-wide k chunks), each followed by the per-agent tail (at three or
+    four waves per SIMD, DOL_MLP_TAIL_OCC).  Cases: d with and without a partial
     last chunk, B < 32, plain and momentum SGD, first steps, write_grad, and a
     shape outside the alternative path (B = 33: falls back)."""
     import os
