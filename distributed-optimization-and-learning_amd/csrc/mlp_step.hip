@@ -835,7 +835,7 @@ __global__ __launch_bounds__(64) void mlp_f1_tile_kernel(MlpArgs a, float* __res
 // agent on ONE XCD (blockIdx % 8 = agent % 8, tiles in order), so the shared
 // lines meet in that XCD's L2.  Same arithmetic per tile: same bits.
 template <int KS, int UPD, bool TH, bool AL, int CH = 1, int XG = 0>
-__global__ __launch_bounds__(kThreads) void mlp_dw1_kernel(MlpArgs a, const float* __restrict__ ws, int n_agents) {
+__device__ __forceinline__ void mlp_dw1_body(MlpArgs a, const float* __restrict__ ws, int n_agents) {
   const int B = a.B, d = a.d, h = a.h, c = a.c;
   const int ndt = (d + 31) / 32;
   int dt, agent;
@@ -922,6 +922,19 @@ __global__ __launch_bounds__(kThreads) void mlp_dw1_kernel(MlpArgs a, const floa
   }
 }
 
+template <int KS, int UPD, bool TH, bool AL, int CH = 1, int XG = 0>
+__global__ __launch_bounds__(kThreads) void mlp_dw1_kernel(MlpArgs a, const float* __restrict__ ws, int n_agents) {
+  mlp_dw1_body<KS, UPD, TH, AL, CH, XG>(a, ws, n_agents);
+}
+
+// dW1 compiled for four waves per SIMD (<= 128 VGPRs + AGPRs; DOL_MLP_DW1_OCC=4):
+// the two-chain kernel needs 98 + 32 and runs three
+template <int KS, int UPD, bool TH, bool AL, int CH, int XG>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void mlp_dw1_occ4_kernel(
+    MlpArgs a, const float* __restrict__ ws, int n_agents) {
+  mlp_dw1_body<KS, UPD, TH, AL, CH, XG>(a, ws, n_agents);
+}
+
 }  // namespace
 
 extern "C" int64_t dol_mlp_step_workspace_bytes(int32_t n_agents, int32_t B, int32_t h) {
@@ -991,6 +1004,7 @@ extern "C" int dol_mlp_step_f32(float* w, int64_t ldw, float* grad, int64_t ldg,
   // alternating pairs on one box (profiles/r03_mlp_dw1_chains.txt) -- the step
   // is not chain-latency bound; DOL_MLP_DW1_CHAINS=1 restores one chain
   static const int dw1_chains = [] { const char* e = getenv("DOL_MLP_DW1_CHAINS"); return e ? atoi(e) : 2; }();
+  static const int dw1_occ4 = [] { const char* e = getenv("DOL_MLP_DW1_OCC"); return e ? atoi(e) == 4 : 0; }();
   // the one-kernel step with W1 resident in registers (mlp_fwd_kernel PH 3;
   // DOL_MLP_FUSED=1).  It reads W1 once (1.75 instead of 2.16 GB per step at 1024
   // agents) but its 400 resident floats per lane leave one workgroup per CU:
@@ -1073,7 +1087,13 @@ extern "C" int dol_mlp_step_f32(float* w, int64_t ldw, float* grad, int64_t ldg,
       if (nt1) fwd(mlp_fwd_kernel<1, U, TH, AL>, lds);
       else fwd(mlp_fwd_kernel<4, U, TH, AL>, lds);
     }
-    if (dw1_xcd)
+    if (dw1_xcd && dw1_occ4 && dw1_chains == 1)
+      hipLaunchKernelGGL((mlp_dw1_occ4_kernel<KS, U, TH, AL, 1, 1>), grid2, block, 0, s, a, ws, n_agents);
+    else if (dw1_xcd && dw1_occ4)
+      hipLaunchKernelGGL((mlp_dw1_occ4_kernel<KS, U, TH, AL, 2, 1>), grid2, block, 0, s, a, ws, n_agents);
+    else if (dw1_xcd && dw1_chains == 1)
+      hipLaunchKernelGGL((mlp_dw1_kernel<KS, U, TH, AL, 1, 1>), grid2, block, 0, s, a, ws, n_agents);
+    else if (dw1_xcd)
       hipLaunchKernelGGL((mlp_dw1_kernel<KS, U, TH, AL, 2, 1>), grid2, block, 0, s, a, ws, n_agents);
     else if (dw1_chains == 2)
       hipLaunchKernelGGL((mlp_dw1_kernel<KS, U, TH, AL, 2>), grid2, block, 0, s, a, ws, n_agents);

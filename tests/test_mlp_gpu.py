@@ -189,7 +189,8 @@ print("ok")
 
 
 _STEP_PATHS = {  # env of each alternative launch path (read once per process: run in children)
-    "base": dict(DOL_MLP_FUSED="0", DOL_MLP_SPLIT_FWD="0", DOL_MLP_F1_TILES="0", DOL_MLP_F1_KW="32", DOL_MLP_TAIL_OCC="3"),
+    "base": dict(DOL_MLP_FUSED="0", DOL_MLP_SPLIT_FWD="0", DOL_MLP_F1_TILES="0", DOL_MLP_F1_KW="32", DOL_MLP_TAIL_OCC="3",
+                 DOL_MLP_DW1_OCC="3", DOL_MLP_DW1_CHAINS="2"),
     "fused": dict(DOL_MLP_FUSED="1"),
     "split": dict(DOL_MLP_SPLIT_FWD="1"),
     "f1tiles4": dict(DOL_MLP_F1_TILES="4"),
@@ -197,6 +198,7 @@ _STEP_PATHS = {  # env of each alternative launch path (read once per process: r
     "f1tiles3kw64": dict(DOL_MLP_F1_TILES="3", DOL_MLP_F1_KW="64", DOL_MLP_TAIL_OCC="4"),
     "f1tiles4kw64": dict(DOL_MLP_F1_TILES="4", DOL_MLP_F1_KW="64"),
     "split_tail4": dict(DOL_MLP_SPLIT_FWD="1", DOL_MLP_TAIL_OCC="4"),
+    "dw1occ4": dict(DOL_MLP_DW1_OCC="4"),
 }
 
 
@@ -214,7 +216,8 @@ def _run_step_child(root, tmp_path, name):
     return torch.load(f, weights_only=True)
 
 
-@pytest.mark.parametrize("path", ["fused", "split", "f1tiles4", "f1tiles5", "f1tiles3kw64", "f1tiles4kw64", "split_tail4"])
+@pytest.mark.parametrize("path", ["fused", "split", "f1tiles4", "f1tiles5", "f1tiles3kw64", "f1tiles4kw64", "split_tail4",
+                                  "dw1occ4"])
 def test_step_paths_bit_identical(path, gpu, tmp_path):
     """Each alternative launch path of the step gives the same parameters,
     momentum, gradients and losses as the default forward + dW1 kernels, bit
