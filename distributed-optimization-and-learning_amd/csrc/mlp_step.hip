@@ -1005,6 +1005,12 @@ extern "C" int dol_mlp_step_f32(float* w, int64_t ldw, float* grad, int64_t ldg,
   // is not chain-latency bound; DOL_MLP_DW1_CHAINS=1 restores one chain
   static const int dw1_chains = [] { const char* e = getenv("DOL_MLP_DW1_CHAINS"); return e ? atoi(e) : 2; }();
   static const int dw1_occ4 = [] { const char* e = getenv("DOL_MLP_DW1_OCC"); return e ? atoi(e) == 4 : 0; }();
+  // diagnostics: unused dynamic LDS per dW1 workgroup, to cap its occupancy (DOL_MLP_DW1_LDS bytes, <= 64 KiB)
+  static const size_t dw1_lds = [] {
+    const char* e = getenv("DOL_MLP_DW1_LDS");
+    const long v = e ? atol(e) : 0;
+    return static_cast<size_t>(v < 0 ? 0 : v > 65536 ? 65536 : v);
+  }();
   // the one-kernel step with W1 resident in registers (mlp_fwd_kernel PH 3;
   // DOL_MLP_FUSED=1).  It reads W1 once (1.75 instead of 2.16 GB per step at 1024
   // agents) but its 400 resident floats per lane leave one workgroup per CU:
@@ -1094,7 +1100,7 @@ extern "C" int dol_mlp_step_f32(float* w, int64_t ldw, float* grad, int64_t ldg,
     else if (dw1_xcd && dw1_chains == 1)
       hipLaunchKernelGGL((mlp_dw1_kernel<KS, U, TH, AL, 1, 1>), grid2, block, 0, s, a, ws, n_agents);
     else if (dw1_xcd)
-      hipLaunchKernelGGL((mlp_dw1_kernel<KS, U, TH, AL, 2, 1>), grid2, block, 0, s, a, ws, n_agents);
+      hipLaunchKernelGGL((mlp_dw1_kernel<KS, U, TH, AL, 2, 1>), grid2, block, dw1_lds, s, a, ws, n_agents);
     else if (dw1_chains == 2)
       hipLaunchKernelGGL((mlp_dw1_kernel<KS, U, TH, AL, 2>), grid2, block, 0, s, a, ws, n_agents);
     else
