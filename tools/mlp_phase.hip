@@ -58,7 +58,7 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
-  const dim3 g2(unsigned((d + 31) / 32 * n));
+  const dim3 g2(unsigned((d + 31) / 32 * ((n + 7) / 8 * 8)));  // the product's dW1 grid (XCD-grouped tiles)
   hipEvent_t e2;
   CHECK(hipEventCreate(&e2));
   if (argc > 2 && argv[2][0] == 'f') {  // the one-kernel step (PH 3): phases F1, F2+CE, B2, B1
@@ -121,12 +121,12 @@ int main(int argc, char** argv) {
   }
   for (int it = 0; it < 3; ++it) {
     hipLaunchKernelGGL((mlp_fwd_kernel<1, 3, false, false>), dim3(n), dim3(kThreads), lds, 0, a, ws);
-    hipLaunchKernelGGL((mlp_dw1_kernel<16, 3, false, false>), g2, dim3(kThreads), 0, 0, a, ws, n);
+    hipLaunchKernelGGL((mlp_dw1_kernel<16, 3, false, false, 2, 1>), g2, dim3(kThreads), 0, 0, a, ws, n);
   }
   CHECK(hipEventRecord(e0));
   hipLaunchKernelGGL((mlp_fwd_kernel<1, 3, false, false>), dim3(n), dim3(kThreads), lds, 0, a, ws);
   CHECK(hipEventRecord(e2));
-  hipLaunchKernelGGL((mlp_dw1_kernel<16, 3, false, false>), g2, dim3(kThreads), 0, 0, a, ws, n);
+  hipLaunchKernelGGL((mlp_dw1_kernel<16, 3, false, false, 2, 1>), g2, dim3(kThreads), 0, 0, a, ws, n);
   CHECK(hipEventRecord(e1));
   CHECK(hipEventSynchronize(e1));
   float ms, ms_fwd;
