@@ -305,6 +305,19 @@ def primal_dual_round(N: int, P: int, world: int, rank: int, device, steps: int,
     return out
 
 
+def _warm(fn, seconds: float = 0.25) -> None:
+    """Run fn() back to back for ~seconds before a short leg is timed: after an
+    idle gap the GPU's clocks take tens of ms to ramp, and a 10-rep leg of
+    ~1 ms calls otherwise lands inside the ramp (split3 at 1024 agents: 1.25
+    ms per round timed from idle, 1.11 ms timed right after other work, same
+    process; tools/dense_heat_probe.py, profiles/r04p_dense_clock_ramp.jsonl)."""
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        for _ in range(4):
+            fn()
+        torch.cuda.synchronize()
+
+
 def _events_ms(fn, reps: int) -> float:
     """Mean ms of `reps` calls of fn() between two events on the current stream."""
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -399,7 +412,7 @@ def dense_mix_round(device, N: int = 1024, P: int = 101770, reps: int = 10):
     Y = torch.empty_like(X)
     work = torch.empty(ops.dense_split3_workspace_bytes(N, N, P, 0), dtype=torch.uint8, device=device)
     ops.mix_dense_split3(W, X, Y, P=P, work=work)
-    torch.cuda.synchronize(device)
+    _warm(lambda: ops.mix_dense_split3(W, X, Y, P=P, work=work))
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
     for _ in range(reps):
@@ -437,7 +450,7 @@ def er_exact_mix_round(device, N: int = 1024, P: int = 101770, reps: int = 10):
         st["plan"] = G.MixingPlan.from_dense(W, dense_kernel="csr", reuse=st["plan"])
     draw()
     st["plan"].apply(X, Y, P=P)
-    torch.cuda.synchronize(device)
+    _warm(lambda: (draw(), st["plan"].apply(X, Y, P=P)))
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
     ev[0].record()
     for _ in range(reps):
@@ -537,7 +550,7 @@ def config5_round(device, N: int = 1024, reps: int = 10):
         rec("mix", 1)
     for _ in range(2):
         one()
-    torch.cuda.synchronize(device)
+    _warm(one)
     t0 = time.perf_counter()
     for k in range(reps):
         one(k)
@@ -554,7 +567,7 @@ def config5_round(device, N: int = 1024, reps: int = 10):
     sim.batch(X, y)
     for _ in range(2):
         sim.round()
-    torch.cuda.synchronize(device)
+    _warm(sim.round)
     t0 = time.perf_counter()
     for _ in range(reps):
         sim.round()
