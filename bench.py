@@ -619,6 +619,12 @@ def main():
     ring.x.normal_(generator=g)
     ring.y.zero_()
 
+    # device warm-up (not a step): ~0.3 s of the ring-pattern copy kernel over the
+    # same rows lifts the clocks out of their idle ramp before the W warm-up steps
+    # (a short timed region that starts cold runs slow: profiles/r04p_dense_clock_ramp.jsonl)
+    from dolhip import ops as _ops
+    _warm(lambda: _ops.stream_copy_rows(ring.x, ring.y, P=P), seconds=0.3)
+    ring.y.zero_()
     _log(f"ring {N} x {P}: warm-up")
     for _ in range(args.warmup):
         ring.step()
