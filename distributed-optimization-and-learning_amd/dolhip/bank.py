@@ -51,12 +51,24 @@ def round_up(x: int, a: int) -> int:
     return (x + a - 1) // a * a
 
 
+LONG_ROW = 1 << 18  # floats (1 MiB rows)
+
+
 def row_stride(P: int) -> int:
     """Leading dimension for P-float agent rows: 256-B aligned, and never a
     multiple of 8 KiB — power-of-two row strides put the rows a tile walks on
     the same HBM channels (ring mix at 8192 x 2^20 on MI355X: 5.57 TB/s with
-    ld = 2^20, 6.14 TB/s with ld = 2^20 + 1024, tools/membench5.hip)."""
+    ld = 2^20, 6.14 TB/s with ld = 2^20 + 1024, tools/membench5.hip).  Rows of
+    >= 1 MiB (r04): an odd multiple of 8 KiB, ld = 2048 (mod 4096) floats.  The
+    ring round at 8192 x 2^20, strides alternating in one process on two boxes
+    (tools/ring_ld_probe.py, profiles/r04q_ring_ld_probe.jsonl): 2^20 + 1024
+    10.94 ms (6.28 TB/s), + 2048 10.64-10.66 ms (6.45), + 3072 11.05-11.08,
+    + 4096 11.9, + 6144 10.65-10.69; the eps = 5 pass over the same rows runs
+    2-3 % slower at + 2048 (10.59 -> 10.87 ms best kernel on one box,
+    12.66 -> 12.86 on the other, profiles/r04q_eps_ld_probe.jsonl)."""
     ld = round_up(max(P, 1), ROW_ALIGN)
+    if ld >= LONG_ROW:
+        return ld + (2048 - ld % 4096) % 4096
     if ld % 2048 == 0:
         ld += 1024
     return ld
