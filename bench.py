@@ -154,14 +154,7 @@ def cpu_baseline(sizes, P: int, seconds: float, full_agents: int):
     # the reference's round is O(N^2) in its Neighbors scan and O(N) in the
     # consensus work: least-squares fit of seconds/round = a N^2 + b N over the
     # samples, evaluated at full_agents (the per-byte `value` ignores the N^2 part)
-    fit = None
-    if len(sizes) >= 2:
-        A = np.array([[n * n, n] for n in sizes], dtype=np.float64)
-        t = np.array([1.0 / per_n[n]["rounds_per_s"] for n in sizes])
-        (a, b), *_ = np.linalg.lstsq(A, t, rcond=None)
-        t_full = a * full_agents ** 2 + b * full_agents
-        if t_full > 0:
-            fit = {"rounds_per_s": 1.0 / t_full, "seconds_per_round": t_full, "a_s_per_agent2": a, "b_s_per_agent": b}
+    fit = _fit_n2_n({n: per_n[n]["rounds_per_s"] for n in sizes}, full_agents) if len(sizes) >= 2 else None
     return {
         "value": value,
         "unit": "rounds/s",
@@ -182,17 +175,25 @@ def cpu_baseline(sizes, P: int, seconds: float, full_agents: int):
 
 
 def _fit_n2_n(samples: dict, n_full: int):
-    """Least-squares seconds/round = a n^2 + b n over {n: rounds_per_s}, at n_full."""
+    """Non-negative least squares seconds/round = a n^2 + b n (a, b >= 0: a
+    round cannot get cheaper with more agents) over {n: rounds_per_s},
+    evaluated at n_full.  Timing noise can no longer push a or b below zero
+    and so move the extrapolated CPU rate either way."""
+    from scipy.optimize import nnls
     ns = sorted(samples)
     A = np.array([[n * n, n] for n in ns], dtype=np.float64)
     t = np.array([1.0 / samples[n] for n in ns])
-    (a, b), *_ = np.linalg.lstsq(A, t, rcond=None)
+    scale = A.max(axis=0)  # column scaling: n^2 and n differ by orders of magnitude
+    coef, resid = nnls(A / scale, t)
+    a, b = coef / scale
     t_full = a * n_full ** 2 + b * n_full
     return {"rounds_per_s": 1.0 / t_full if t_full > 0 else None, "seconds_per_round": t_full,
-            "a_s_per_agent2": a, "b_s_per_agent": b}
+            "a_s_per_agent2": float(a), "b_s_per_agent": float(b), "residual_s": float(resid),
+            "samples": {int(n): float(1.0 / samples[n]) for n in ns}}
 
 
-def cpu_secondaries(P: int, full_agents: int, admm_sizes=(64, 256), cfg5_sizes=(128, 256), cfg5_agents: int = 1024):
+def cpu_secondaries(P: int, full_agents: int, admm_sizes=(64, 256), cfg5_sizes=(64, 128, 256),
+                    cfg5_agents: int = 1024):
     """CPU legs beside the secondaries (reference-structured torch-CPU code in
     oracle/ref_cpu.py, same threads as cpu_baseline):
       * FedADMM: FedAdmm_Client.update_weights (autograd least-squares loss +
@@ -204,8 +205,9 @@ def cpu_secondaries(P: int, full_agents: int, admm_sizes=(64, 256), cfg5_sizes=(
         SGD momentum, batch 32; DIST/clients.py:34-59) + the consensus round
         with a new ER p = 0.1 W (Neighbors scan + consensus + load_state_dict);
         the local steps grow as n and Neighbors + consensus as n^2, so `value`
-        = the least-squares fit seconds/round = a n^2 + b n over the samples,
-        evaluated at cfg5_agents.
+        = the non-negative least-squares fit seconds/round = a n^2 + b n over
+        the three samples, evaluated at cfg5_agents (the largest sample's rate
+        scaled by (n / cfg5_agents)^2, the r03 bound, is reported beside it).
     Every size runs a warm-up round, then 2 timed rounds."""
     from oracle import ref_cpu
     threads = torch.get_num_threads()
@@ -222,8 +224,9 @@ def cpu_secondaries(P: int, full_agents: int, admm_sizes=(64, 256), cfg5_sizes=(
         c5[n] = {"rounds": r, "seconds": sec, "rounds_per_s": r / sec}
     b5 = max(cfg5_sizes)
     fit5 = _fit_n2_n({n: v["rounds_per_s"] for n, v in c5.items()}, cfg5_agents)
+    fit5["n2_bound_rounds_per_s"] = c5[b5]["rounds_per_s"] * (b5 / cfg5_agents) ** 2
     if fit5["rounds_per_s"] is None:  # degenerate samples: the per-byte-squared bound instead
-        fit5["rounds_per_s"] = c5[b5]["rounds_per_s"] * (b5 / cfg5_agents) ** 2
+        fit5["rounds_per_s"] = fit5["n2_bound_rounds_per_s"]
     return {
         "fedadmm": {"value": adm[big]["rounds_per_s"] * big / full_agents, "unit": "rounds/s", "cores": threads,
                     "kind": "port", "per_clients": adm,
@@ -234,7 +237,7 @@ def cpu_secondaries(P: int, full_agents: int, admm_sizes=(64, 256), cfg5_sizes=(
                     "kind": "port", "per_agents": c5, "fit_a_n2_plus_b_n": fit5,
                     "sample": f"reference-structured torch-CPU config-5 round (oracle/ref_cpu.py "
                               f"time_config5_rounds: per-agent nn.Module MLP step + ER W Neighbors/consensus), n in "
-                              f"{list(cfg5_sizes)}, warm-up + 2 rounds each; value = the least-squares fit "
+                              f"{list(cfg5_sizes)}, warm-up + 2 rounds each; value = the non-negative least-squares fit "
                               f"seconds/round = a n^2 + b n evaluated at n={cfg5_agents}"},
     }
 

@@ -3,6 +3,17 @@
 
 #include <stdint.h>
 
+// The LDS-DMA pipelines (ring_mix_dma / ring_stream_dma / csr_pm / csr_slab /
+// the MLP step) retire their loads with counted `s_waitcnt vmcnt(N)` waits
+// that also count the buffer stores issued in between, in issue order, and
+// the dropped (out-of-range) stores are counted too.  That holds on gfx9
+// (one vector-memory counter); targets with a separate store counter (vscnt)
+// would make every counted wait wrong.  Device code is built for gfx950 only
+// (tests/test_codegen_pins.py pins the emitted waits).
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "libdol_hip's counted vmcnt pipelines are written for gfx950 (one counter for loads and stores)"
+#endif
+
 namespace dol {
 // Every size / leading dimension an entry point accepts is at most 2^40
 // elements (4 TiB of fp32, far above one GPU's 288 GB), so no byte or block

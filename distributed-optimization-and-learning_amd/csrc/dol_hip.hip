@@ -1464,8 +1464,13 @@ int dol_version(void) { return 100; }
 
 const char* dol_last_error(void) { return g_err; }
 
-static std::mutex g_bank_mu;  // dol_bank_alloc's live blocks: VA -> physical handle
-static std::unordered_map<void*, hipMemGenericAllocationHandle_t> g_bank_handles;
+struct BankBlock {
+  hipMemGenericAllocationHandle_t handle;
+  size_t size;    // the mapped (granularity-rounded) size: what unmap / address-free take
+  int stage = 0;  // 0 mapped, 1 unmapped, 2 range freed (dol_bank_free resumes from here)
+};
+static std::mutex g_bank_mu;  // dol_bank_alloc's live blocks: VA -> physical handle + mapped size
+static std::unordered_map<void*, BankBlock> g_bank_handles;
 
 // A bank buffer as ONE physical allocation (hipMemCreate) mapped into a
 // reserved VA range, instead of whatever hipMalloc's suballocator returns
@@ -1509,7 +1514,7 @@ int dol_bank_alloc(int64_t bytes, void** ptr, int64_t* mapped_bytes) {
   }
   {  // the handle lives until dol_bank_free has unmapped the range (create, map ... unmap, release)
     std::lock_guard<std::mutex> lk(g_bank_mu);
-    g_bank_handles[va] = h;
+    g_bank_handles[va] = BankBlock{h, size};
   }
   *ptr = va;
   *mapped_bytes = static_cast<int64_t>(size);
@@ -1517,21 +1522,33 @@ int dol_bank_alloc(int64_t bytes, void** ptr, int64_t* mapped_bytes) {
   return DOL_OK;
 }
 
+// Unmap, free the range, release the handle -- with the size recorded at
+// allocation (mapped_bytes must match it).  The entry is erased only after all
+// three succeed, so a failed step leaves the block registered and a later call
+// retries from that step.
 int dol_bank_free(void* ptr, int64_t mapped_bytes) {
   if (!ptr) return DOL_OK;
-  if (mapped_bytes <= 0 || mapped_bytes > 8 * dol::kMaxDim) return fail(DOL_EINVAL, "dol_bank_free: bad size");
-  hipMemGenericAllocationHandle_t h{};
-  {
-    std::lock_guard<std::mutex> lk(g_bank_mu);
-    auto it = g_bank_handles.find(ptr);
-    if (it == g_bank_handles.end()) return fail(DOL_EINVAL, "dol_bank_free: %p is not a dol_bank_alloc block", ptr);
-    h = it->second;
-    g_bank_handles.erase(it);
+  std::lock_guard<std::mutex> lk(g_bank_mu);
+  auto it = g_bank_handles.find(ptr);
+  if (it == g_bank_handles.end()) return fail(DOL_EINVAL, "dol_bank_free: %p is not a dol_bank_alloc block", ptr);
+  BankBlock& blk = it->second;
+  if (mapped_bytes != static_cast<int64_t>(blk.size))
+    return fail(DOL_EINVAL, "dol_bank_free: size %lld differs from the mapped %zu bytes",
+                static_cast<long long>(mapped_bytes), blk.size);
+  hipError_t e = hipSuccess;
+  if (blk.stage == 0) {
+    if ((e = hipMemUnmap(ptr, blk.size)) != hipSuccess)
+      return fail(-static_cast<int>(e), "dol_bank_free: hipMemUnmap: %s", hipGetErrorString(e));
+    blk.stage = 1;
   }
-  hipError_t e = hipMemUnmap(ptr, static_cast<size_t>(mapped_bytes));
-  if (e == hipSuccess) e = hipMemAddressFree(ptr, static_cast<size_t>(mapped_bytes));
-  if (e == hipSuccess) e = hipMemRelease(h);
-  if (e != hipSuccess) return fail(-static_cast<int>(e), "dol_bank_free: %s", hipGetErrorString(e));
+  if (blk.stage == 1) {
+    if ((e = hipMemAddressFree(ptr, blk.size)) != hipSuccess)
+      return fail(-static_cast<int>(e), "dol_bank_free: hipMemAddressFree: %s", hipGetErrorString(e));
+    blk.stage = 2;
+  }
+  if ((e = hipMemRelease(blk.handle)) != hipSuccess)
+    return fail(-static_cast<int>(e), "dol_bank_free: hipMemRelease: %s", hipGetErrorString(e));
+  g_bank_handles.erase(it);
   g_err[0] = '\0';
   return DOL_OK;
 }

@@ -89,14 +89,45 @@ class _MappedBlock:
         self.__cuda_array_interface__ = {"shape": (rows, cols), "typestr": "<f4", "data": (self.ptr, False),
                                          "version": 2, "strides": None}
 
+    def release(self) -> None:
+        """Wait for the device, then unmap and release the block; raises
+        DolNativeError (with dol_last_error) if a step fails -- the block then
+        stays registered and release() can be called again."""
+        if not getattr(self, "ptr", 0):
+            return
+        torch.cuda.synchronize(self.device)  # no kernel may still use the block
+        _native.call("dol_bank_free", self.ptr, self.mapped)
+        self.ptr = 0
+
     def __del__(self):
-        if getattr(self, "ptr", 0):
-            try:
-                torch.cuda.synchronize(self.device)  # no kernel may still use the block
-                _native.lib().dol_bank_free(self.ptr, self.mapped)
-            except Exception:  # noqa: BLE001 - interpreter teardown
-                pass
-            self.ptr = 0
+        if not getattr(self, "ptr", 0):
+            return
+        try:
+            self.release()
+        except Exception as e:  # noqa: BLE001 - a destructor cannot raise; say so instead of leaking silently
+            import sys
+            import warnings
+            if sys is not None and not sys.is_finalizing():
+                warnings.warn(f"dolhip: a mapped bank block of {self.mapped} bytes at {self.ptr:#x} was not "
+                              f"released ({type(e).__name__}: {e}); it stays allocated", ResourceWarning,
+                              stacklevel=2)
+            _LEAKED.append(self)  # keep the registration reachable for a later retry (release_leaked)
+
+
+_LEAKED: List["_MappedBlock"] = []
+
+
+def release_leaked() -> int:
+    """Retry the release of mapped blocks whose destructor failed; returns how
+    many are still held."""
+    keep = []
+    for blk in _LEAKED:
+        try:
+            blk.release()
+        except Exception:  # noqa: BLE001 - still failing: keep it
+            keep.append(blk)
+    _LEAKED[:] = keep
+    return len(keep)
 
 
 MAPPED_MIN_BYTES = 1 << 30

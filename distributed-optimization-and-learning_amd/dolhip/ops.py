@@ -124,7 +124,7 @@ def mix_csr_pm(XT: torch.Tensor, YT: torch.Tensor, rowptr: torch.Tensor, col: to
 
 def _pm_auto(XT, YT, ldx, ldy, x_agents, n, P, launch) -> int:
     key = _pair_key("pm", XT, YT, ldx, ldy, x_agents, n, P)
-    return _auto_choice(key, launch, PM_STAGE_ORDERS, (x_agents + n) * P * 4)
+    return _auto_choice(key, launch, PM_STAGE_ORDERS, (x_agents + n) * P * 4, XT.device)
 
 
 def pm_stage_order(nseg: int) -> int:
@@ -157,20 +157,26 @@ def ring_steps_variant(variant: int) -> int:
     return rc
 
 
-def _time_each(run_with, candidates, reps):
-    """{candidate: mean ms of `reps` calls of run_with(candidate)} on the current stream."""
-    dev = torch.cuda.current_device()
+def _time_each(run_with, candidates, reps, device=None):
+    """{candidate: mean ms of `reps` calls of run_with(candidate)} on the
+    current stream of `device` (default: the current device) -- the stream the
+    ops launch on for tensors there.  Events bracket the calls on that stream
+    and the host waits on the closing event only: no device-wide
+    synchronisation, so work on other streams (a side stream's W draw, another
+    rank's buffers) is neither waited for nor serialised."""
+    device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
     times = {}
-    for c in candidates:
-        run_with(c)
-        torch.cuda.synchronize(dev)
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record()
-        for _ in range(reps):
-            run_with(c)
-        e.record()
-        torch.cuda.synchronize(dev)
-        times[c] = s.elapsed_time(e) / reps
+    with torch.cuda.device(device):
+        stream = torch.cuda.current_stream(device)
+        for c in candidates:
+            run_with(c)  # warm (first launch of this variant on these buffers)
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record(stream)
+            for _ in range(reps):
+                run_with(c)
+            e.record(stream)
+            e.synchronize()
+            times[c] = s.elapsed_time(e) / reps
     return times
 
 
@@ -220,15 +226,20 @@ def tuned_choices() -> dict:
     return {repr(k): dict(v) for k, v in _TUNED.items()}
 
 
-def _auto_choice(key, run_with, candidates, nbytes: int) -> int:
+def _auto_choice(key, run_with, candidates, nbytes: int, device) -> int:
+    """The cached pick for `key`, or time every candidate on `device`'s current
+    stream (where the buffers live and the ops launch), cache and return the
+    fastest; 0 (the library default) when tuning is off, the buffers are small
+    or that stream is being captured into a graph."""
     if not autotune_enabled() or nbytes < AUTOTUNE_MIN_BYTES:
         return 0
     hit = _TUNED.get(key)
     if hit is not None:
         return hit["choice"]
-    if torch.cuda.is_current_stream_capturing():  # no timing inside a graph capture
-        return 0
-    times = _time_each(run_with, candidates, AUTOTUNE_REPS)
+    with torch.cuda.device(device):
+        if torch.cuda.is_current_stream_capturing():  # no timing inside a graph capture
+            return 0
+    times = _time_each(run_with, candidates, AUTOTUNE_REPS, device=device)
     best = min(times, key=times.get)
     _TUNED[key] = {"choice": best, "ms": times}
     return best
@@ -395,7 +406,7 @@ def mix_ring_steps(X: torch.Tensor, Y: torch.Tensor, w_prev: torch.Tensor, w_nex
                      w_prev.data_ptr(), w_next.data_ptr(), int(v), _stream(X))
     if variant is None:
         variant = _auto_choice(_pair_key("ring_steps", X, Y, ldx, ldy, n, P, int(steps)), launch,
-                               RING_STEPS_VARIANTS, 2 * n * P * 4) if steps > 1 else 0
+                               RING_STEPS_VARIANTS, 2 * n * P * 4, X.device) if steps > 1 else 0
     launch(variant)
     return Y
 

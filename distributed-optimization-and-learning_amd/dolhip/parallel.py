@@ -19,9 +19,10 @@ contiguous blocks, one block per rank:
   one GPU: every column's arithmetic is unchanged.
 * global mean (FedAvg / FedProx / FedADMM server average): each rank sums its
   local sampled rows in sampled order, then `all_reduce(SUM)` and a division
-  by m ("fast", association order differs from the reference by rank), or an
-  ordered chain over ranks in the global sampled order ("exact": bit-identical
-  to DEC/servers.py:42-48, one hop per change of owner).
+  by m ("fast", association order differs from the reference by rank), or
+  ("exact": bit-identical to DEC/servers.py:42-48) one all_to_all of the
+  sampled rows to parameter-column blocks, an ordered sum in the global
+  sampled order per block, and one all_gather of theta.
 """
 from __future__ import annotations
 
@@ -478,11 +479,49 @@ def global_mean(local_rows: torch.Tensor, local_order: Sequence[int], m_total: i
     return ordered_sum(None, zero, acc_in=out, out=out, scale=float(m_total), P=P)
 
 
+def exact_mean_plan(order: Sequence[int], bounds: Sequence[Tuple[int, int]], P: int, world: int, rank: int):
+    """Host bookkeeping of global_mean_exact (pure numpy; the gloo tests and the
+    GPU path share it).  Returns (mine, counts, perm, cols):
+      mine   this rank's sampled rows (LOCAL indices) in global sampled order;
+      counts sampled agents owned by each rank;
+      perm   perm[k] = row of the k-th sampled agent in the received block
+             (sources in rank order, each source's rows in global order);
+      cols   the parameter-column blocks column_bounds(P, world, q)."""
+    import numpy as np
+    order = np.asarray(order, dtype=np.int64).reshape(-1)
+    his = np.asarray([b for _, b in bounds], dtype=np.int64)
+    los = np.asarray([a for a, _ in bounds], dtype=np.int64)
+    owner = np.searchsorted(his, order, side="right")
+    if order.size and (owner.max() >= world or np.any(order < los[np.minimum(owner, world - 1)])):
+        raise ValueError("global_mean_exact: a sampled agent lies outside every rank's rows")
+    counts = np.bincount(owner, minlength=world).astype(np.int64)
+    within = np.empty(order.size, dtype=np.int64)
+    for q in range(world):
+        sel = np.nonzero(owner == q)[0]
+        within[sel] = np.arange(sel.size)
+    offs = np.concatenate([[0], np.cumsum(counts)[:-1]])
+    perm = (offs[owner] + within).astype(np.int32)
+    mine = order[owner == rank] - bounds[rank][0]
+    cols = [column_bounds(P, world, q) for q in range(world)]
+    return mine, counts, perm, cols
+
+
 def global_mean_exact(local_rows: torch.Tensor, lo: int, hi: int, order: Sequence[int], P: int,
                       group=None, out: Optional[torch.Tensor] = None, ordered_sum=None) -> torch.Tensor:
-    """Bit-exact DEC/servers.py:42-48 order across ranks: the running sum hops
-    to the owner of each run of consecutive sampled agents, then is broadcast
-    from the last owner.  `order` holds GLOBAL agent ids; rows [lo, hi) local."""
+    """Bit-exact DEC/servers.py:42-48 across ranks with O(1) collectives.
+
+    average_weights adds the sampled clients' rows one after another in the
+    sampled order, then divides by m, and each column's sum is independent of
+    every other column.  So the sampled rows move once, to parameter-column
+    blocks: one all_to_all sends rank q the columns column_bounds(P, world, q)
+    of this rank's sampled rows, each rank adds its column block's m rows in
+    the GLOBAL sampled order (ops.ordered_sum over a permutation of the
+    received block: the reference's association order, + then / m in one
+    pass), and one all_gather assembles theta on every rank.  Every element of
+    theta is the same fp32 computation as on one GPU, whatever the world size.
+    Traffic per rank: its own sampled rows once (an all_reduce would move the
+    [P] sum twice, but in a rank-dependent association order: `global_mean`).
+    `order` holds GLOBAL agent ids; rows [lo, hi) are local."""
     ordered_sum = ordered_sum if ordered_sum is not None else ops.ordered_sum
     device = local_rows.device
     world = dist.get_world_size(group) if dist.is_initialized() else 1
@@ -490,48 +529,66 @@ def global_mean_exact(local_rows: torch.Tensor, lo: int, hi: int, order: Sequenc
     m = len(order)
     if m < 1:
         raise ValueError("need at least one sampled agent")
-    bounds = [(lo, hi)] if world == 1 else _all_bounds(lo, hi, device, group)
-    owner = [next(r for r, (a, b) in enumerate(bounds) if a <= g < b) for g in order]
-    runs: List[Tuple[int, List[int]]] = []
-    for g, o in zip(order, owner):
-        if runs and runs[-1][0] == o:
-            runs[-1][1].append(g)
-        else:
-            runs.append((o, [g]))
     acc = out if out is not None else torch.empty(P, dtype=torch.float32, device=device)
-    have = False
-    for k, (o, ids) in enumerate(runs):
-        if o == rank:
-            if k > 0 and runs[k - 1][0] != rank:
-                _p2p(dist.recv, acc[:P], runs[k - 1][0], group)
-                have = True
-            idx = torch.as_tensor([g - lo for g in ids], dtype=torch.int32, device=device)
-            last = k == len(runs) - 1
-            ordered_sum(local_rows, idx, acc_in=acc if have else None, out=acc,
-                            scale=float(m) if last else 1.0, P=P)
-            have = True
-            if not last and runs[k + 1][0] != rank:
-                _p2p(dist.send, acc[:P], runs[k + 1][0], group)
-    if world > 1:
-        _p2p(dist.broadcast, acc[:P], runs[-1][0], group)
+    if world == 1:
+        if min(order) < lo or max(order) >= hi:
+            raise ValueError("global_mean_exact: a sampled agent lies outside the local rows")
+        idx = torch.as_tensor([int(g) - lo for g in order], dtype=torch.int32, device=device)
+        return ordered_sum(local_rows, idx, out=acc, scale=float(m), P=P)
+    bounds = _all_bounds(lo, hi, device, group)
+    mine, counts, perm, cols = exact_mean_plan(order, bounds, P, world, rank)
+    c0, c1 = cols[rank]
+    Pc, m_me = c1 - c0, int(mine.size)
+    # pack: to rank q, my sampled rows (global order) x q's columns, contiguous
+    send = torch.empty(max(m_me * P, 1), dtype=torch.float32, device=device)
+    if m_me:
+        sel = torch.as_tensor(mine, dtype=torch.int64, device=device)
+        off = 0
+        for a, b in cols:
+            if b > a:
+                torch.index_select(local_rows[:, a:b], 0, sel, out=send[off:off + m_me * (b - a)].view(m_me, b - a))
+            off += m_me * (b - a)
+    recv = torch.empty(max(m * Pc, 1), dtype=torch.float32, device=device)
+    _all_to_all(recv, send, [int(counts[s]) * Pc for s in range(world)], [m_me * (b - a) for a, b in cols], group)
+    pmax = max(b - a for a, b in cols)
+    part = torch.zeros(max(pmax, 1), dtype=torch.float32, device=device)
+    if Pc > 0:
+        idx = torch.as_tensor(perm, dtype=torch.int32, device=device)
+        ordered_sum(recv[:m * Pc].view(m, Pc), idx, out=part, scale=float(m), P=Pc)
+    parts = _all_gather(part, group)
+    for q, (a, b) in enumerate(cols):
+        if b > a:
+            acc[a:b].copy_(parts[q][:b - a])
     return acc
+
+
+def _all_to_all(recv: torch.Tensor, send: torch.Tensor, recv_splits, send_splits, group) -> None:
+    """all_to_all_single over the first sum(splits) elements (gloo: staged through host memory)."""
+    ns, nr = int(sum(send_splits)), int(sum(recv_splits))
+    if _gloo_staged(send, group):
+        hs, hr = send[:ns].cpu(), torch.empty(nr, dtype=recv.dtype)
+        dist.all_to_all_single(hr, hs, list(recv_splits), list(send_splits), group=group)
+        recv[:nr].copy_(hr)
+    else:
+        dist.all_to_all_single(recv[:nr], send[:ns], list(recv_splits), list(send_splits), group=group)
+
+
+def _all_gather(t: torch.Tensor, group) -> List[torch.Tensor]:
+    """Every rank's `t` (equal sizes), in rank order (gloo: staged through host memory)."""
+    world = dist.get_world_size(group)
+    if dist.get_backend(group) == "gloo":
+        src = t.cpu() if t.device.type == "cuda" else t
+        outs = [torch.empty_like(src) for _ in range(world)]
+        dist.all_gather(outs, src, group=group)
+        return [o.to(t.device) for o in outs] if t.device.type == "cuda" else outs
+    flat = torch.empty(world * t.numel(), dtype=t.dtype, device=t.device)
+    dist.all_gather_into_tensor(flat, t, group=group)
+    return list(flat.view(world, t.numel()))
 
 
 def _gloo_staged(t: torch.Tensor, group) -> bool:
     """gloo reads raw host pointers: device tensors go through host memory."""
     return t.device.type == "cuda" and dist.get_backend(group) == "gloo"
-
-
-def _p2p(fn, t: torch.Tensor, peer: int, group) -> None:
-    """dist.send / dist.recv / dist.broadcast of `t` with `peer` (dst / src),
-    staged through a host copy under gloo."""
-    if not _gloo_staged(t, group):
-        fn(t, peer, group=group)
-        return
-    host = t.cpu()
-    fn(host, peer, group=group)
-    if fn is not dist.send:
-        t.copy_(host)
 
 
 def _all_bounds(lo: int, hi: int, device, group=None) -> List[Tuple[int, int]]:

@@ -452,9 +452,12 @@ int dol_er_stochastic_f32(float* W, int64_t ldw, int32_t n, float p, uint64_t se
  * Device memory for a bank buffer as ONE physical allocation (hipMemCreate)
  * mapped into a reserved virtual range (hipMemAddressReserve + hipMemMap),
  * rounded up to the allocation granularity (*mapped_bytes).  Free with
- * dol_bank_free(ptr, *mapped_bytes), which unmaps the range and then
- * releases the physical allocation; it refuses a pointer this library did not
- * hand out (DOL_EINVAL, before any HIP call) and accepts NULL.  Host-side,
+ * dol_bank_free(ptr, *mapped_bytes), which unmaps the range, frees it and
+ * then releases the physical allocation, with the size recorded at allocation;
+ * it refuses a pointer this library did not hand out or a size other than
+ * *mapped_bytes (DOL_EINVAL, before any HIP call) and accepts NULL.  A failed
+ * step leaves the block registered: calling dol_bank_free again resumes at
+ * that step.  Host-side,
  * synchronous, thread-safe, not graph-capturable.  Opt-in for bank buffers
  * (bank.device_matrix, DOL_BANK_ALLOC=vmm).  No reference counterpart (the
  * reference keeps one nn.Module per agent in host memory).

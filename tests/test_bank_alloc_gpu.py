@@ -41,6 +41,72 @@ def test_mapped_matrix_round_trip_and_mix(gpu, monkeypatch):
     torch.cuda.synchronize()
 
 
+def _remap_cycle(gpu, n, P, plan_csr, k, check):
+    """One cycle of the r04 fault's sequence on fresh exact-size mapped blocks:
+    map X / Y / T / M, fill them with torch (normal_ / zero_), run every bank
+    kernel on the LAST rows (row views ending at the block's last byte), free."""
+    ld = B.row_stride(P)
+    assert (n * ld * 4) % (2 << 20) == 0  # the data ends exactly where the mapping ends
+    X, Y, T, M = (B.device_matrix(n, ld, gpu, mapped=True) for _ in range(4))
+    g = torch.Generator(device=gpu).manual_seed(100 + k)
+    X.normal_(generator=g)
+    T.normal_(generator=g)
+    M.zero_()
+    Y.zero_()
+    w = torch.rand(n, generator=g, device=gpu)
+    wn = 1.0 - w
+    rp, col, val = plan_csr
+    # config 3's DGD rounds (ring, then random-regular CSR), first step then continuing momentum
+    for first in (True, False):
+        ops.dgd_ring(X, Y, w, wn, T, mom=M, steps=2, lr=0.01, momentum=0.5, first_step=first, P=P)
+        ops.dgd_csr(Y, X, rp, col, val, T, mom=M, steps=1, lr=0.01, momentum=0.5, first_step=False, P=P)
+    # the last rows as a sharded block: interior mix with halo rows + both edges
+    t = 3
+    hp, hn = X[n - t - 1, :P].contiguous(), X[0, :P].contiguous()
+    ops.mix_ring(X[n - t:], Y[n - t:], w[n - t:], wn[n - t:], halo_prev=hp, halo_next=hn, P=P)
+    ops.mix_ring_edges(X[n - t:], Y[n - t:], w[n - t:], wn[n - t:], hp, hn, P=P)
+    # FedLCon's eps pass under every kernel the tuner may pick, the ordered mean, the ADMM / dual / prox updates
+    P4 = P // 4 * 4
+    for v in ops.RING_STEPS_VARIANTS:
+        ops.mix_ring_steps(X, Y, w, wn, 5, P=P4, n_rows=n, variant=v)
+    order = torch.arange(n - 1, n - 9, -1, dtype=torch.int32, device=gpu)
+    theta = ops.ordered_mean(X, order, P=P)
+    ops.admm_ls_round(X, M, T, theta, agents=order, first=torch.zeros(8, dtype=torch.int32, device=gpu), buf=Y,
+                      rho=0.1, lr=0.1, momentum=0.5, local_steps=2, P=P)
+    ops.admm_dual(M[n - 2:], X[n - 2:], theta, 0.1, P=P)
+    ops.prox_admm_sgd(X[n - 2:], T[n - 2:], buf=Y[n - 2:], theta=theta, alpha=M[n - 2:], rho=0.1, lr=0.1,
+                      momentum=0.5, first_step=False, P=P)
+    torch.cuda.synchronize()
+    if check:  # the last row's mix after everything above, against the oracle
+        Xl = X[n - 3:, :P].cpu().numpy()
+        ops.mix_ring(X[n - 3:], Y[n - 3:], w[n - 3:], wn[n - 3:], halo_prev=hp, halo_next=hn, P=P)
+        torch.cuda.synchronize()
+        want = oracle.mix_ring(Xl, w[n - 3:].cpu().numpy(), wn[n - 3:].cpu().numpy(), hp.cpu().numpy(),
+                               hn.cpu().numpy())
+        assert bits_equal(Y[n - 3:, :P].cpu().numpy(), want)
+    del X, Y, T, M, hp, hn, theta
+    gc.collect()
+    torch.cuda.synchronize()
+
+
+def test_mapped_blocks_survive_map_free_remap_cycles(gpu):
+    """the r04k fault came after a process had mapped and
+    freed seven 4 GiB dol_bank_alloc blocks.  Twelve cycles of exact-size
+    mapped blocks (512 rows x (2^20 - 5) floats, ld 2^20 + 2048: 2 GiB + 4 MiB
+    each, ending on the mapping's last byte) with every bank kernel on their
+    last rows, freed and re-mapped each cycle (the host restatement of these
+    kernels' extents is tests/test_kernel_extents.py)."""
+    from dolhip import graph as G
+    n, P = 512, (1 << 20) - 5
+    c = G.random_regular_csr(n, 4, seed=2028)
+    csr = (torch.as_tensor(np.asarray(c.rowptr, np.int32), device=gpu),
+           torch.as_tensor(np.asarray(c.col, np.int32), device=gpu),
+           torch.as_tensor(np.asarray(c.val, np.float32), device=gpu))
+    for k in range(12):
+        _remap_cycle(gpu, n, P, csr, k, check=(k in (0, 11)))
+    assert B.release_leaked() == 0
+
+
 def test_bank_maps_large_state_when_asked(gpu, monkeypatch):
     made = []
 

@@ -33,6 +33,20 @@ def test_fit_n2_n_linear_cost_is_not_squared(bench):
     assert fit["rounds_per_s"] == pytest.approx(1.0 / (1e-3 * 1024), rel=1e-6)
 
 
+def test_fit_n2_n_noise_cannot_make_a_coefficient_negative(bench):
+    """with samples whose exact solve has b < 0 (the middle size
+    slow, the largest fast), the fit stays in a, b >= 0 and the extrapolated
+    rate stays positive and finite."""
+    samples = {64: 1.0 / 0.010, 128: 1.0 / 0.030, 256: 1.0 / 0.050}
+    fit = bench._fit_n2_n(samples, 1024)
+    assert fit["a_s_per_agent2"] >= 0.0 and fit["b_s_per_agent"] >= 0.0
+    assert fit["rounds_per_s"] is not None and 0 < fit["rounds_per_s"] < samples[256]
+    # a pure n^2 cost with one noisy point: a > 0 and a rate below the largest sample's
+    noisy = {64: 1.0 / (1e-6 * 64 ** 2), 128: 1.0 / (1e-6 * 128 ** 2 * 1.2), 256: 1.0 / (1e-6 * 256 ** 2 * 0.9)}
+    f2 = bench._fit_n2_n(noisy, 1024)
+    assert f2["a_s_per_agent2"] > 0 and f2["b_s_per_agent"] >= 0 and f2["rounds_per_s"] < noisy[256]
+
+
 def test_every_ring_steps_variant_has_a_kernel_name(bench):
     import sys
     sys.path.insert(0, os.path.join(ROOT, "distributed-optimization-and-learning_amd"))

@@ -1,0 +1,84 @@
+"""Pins on the emitted gfx950 code of the counted-wait LDS-DMA kernels (CPU
+tier: reads the code object hipcc built, runs nothing).
+
+ring_stream_dma_kernel<S, D, PF, ...> (FedLCon's eps pass, variants 3-5 of
+dol_mix_ring_steps_ex_f32) is bit-exact only if every `s_waitcnt vmcnt(N)` it
+executes retires exactly the LDS-DMA row about to be read.  Its accounting
+ assumes one vector-memory counter that counts loads AND
+buffer stores in issue order, with every dropped prologue / tail store
+actually issued.  A compiler that merged the dropped stores, moved a wait,
+or a target that counts stores separately (vscnt) breaks it silently, so the
+code object is checked here:
+  * every vmcnt wait in the kernel is vmcnt(2D - 2) (the steady state) or
+    vmcnt(0) (the final drain);
+  * no s_waitcnt_vscnt (gfx9: one counter; dol_common.h refuses non-gfx950
+    device builds);
+  * both bodies' prologue stores survive dead-store elimination (>= 2 (D - 1)
+    buffer stores; the volatile bit + distinct out-of-range offsets).
+"""
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "distributed-optimization-and-learning_amd", "csrc")
+LLVM = "/opt/rocm/lib/llvm/bin"
+
+
+@pytest.fixture(scope="module")
+def code_object(tmp_path_factory):
+    obj = os.path.join(CSRC, "obj", "dol_hip.o")
+    if not os.path.exists(obj):
+        subprocess.run(["make", "-s", "-C", CSRC, "obj/dol_hip.o"], check=True)
+    bundler = os.path.join(LLVM, "clang-offload-bundler")
+    if not os.path.exists(bundler):
+        pytest.skip("clang-offload-bundler not found")
+    d = tmp_path_factory.mktemp("co")
+    fat, co = str(d / "fat.bin"), str(d / "co.o")
+    subprocess.run(["objcopy", "--dump-section", f".hip_fatbin={fat}", obj], check=True)
+    subprocess.run([bundler, "--type=o", "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--input={fat}",
+                    f"--output={co}", "--unbundle"], check=True)
+    return co
+
+
+def _kernels(co, stem):
+    out = subprocess.run([os.path.join(LLVM, "llvm-objdump"), "-t", co], check=True, capture_output=True,
+                         text=True).stdout
+    names = {ln.split()[-1] for ln in out.splitlines() if stem in ln}
+    return sorted(n for n in names if not re.search(r"\.(kd|private_seg_size|num_\w+|uses_\w+|has_\w+|numbered_\w+)$", n))
+
+
+def _disasm(co, sym):
+    return subprocess.run([os.path.join(LLVM, "llvm-objdump"), "-d", f"--disassemble-symbols={sym}", co],
+                          check=True, capture_output=True, text=True).stdout
+
+
+def test_ring_stream_dma_waits_are_counted(code_object):
+    ks = _kernels(code_object, "ring_stream_dma_kernel")
+    assert ks, "no ring_stream_dma_kernel instantiations in the code object"
+    for k in ks:
+        m = re.search(r"ring_stream_dma_kernelILi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELb([01])E", k)
+        assert m, k
+        S, D, PF, probe, sync = map(int, m.groups())
+        asm = _disasm(code_object, k)
+        waits = [int(v) for v in re.findall(r"s_waitcnt vmcnt\((\d+)\)", asm)]
+        assert waits, f"{k}: no vmcnt waits"
+        assert set(waits) <= {2 * D - 2, 0}, f"{k}: unexpected waits {sorted(set(waits))} (expected {2 * D - 2} / 0)"
+        assert waits.count(2 * D - 2) >= PF, f"{k}: the steady-state wait is missing"
+        assert "vscnt" not in asm, f"{k}: a separate store counter breaks the counted waits"
+        stores = len(re.findall(r"buffer_store_dwordx4", asm))
+        assert stores >= 2 * (D - 1), f"{k}: only {stores} buffer stores (dropped prologue stores merged?)"
+        assert len(re.findall(r"global_load_lds_dwordx4", asm)) >= D, f"{k}: DMA loads missing"
+
+
+def test_device_build_refuses_other_targets():
+    """dol_common.h stops a device build for a target other than gfx950."""
+    hipcc = "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("hipcc not found")
+    src = '#include "dol_common.h"\n__global__ void k(float* p) { p[0] = 1.0f; }\n'
+    r = subprocess.run([hipcc, "--offload-arch=gfx942", "--cuda-device-only", "-c", "-x", "hip", "-", "-I", CSRC,
+                        "-o", os.devnull], input=src, capture_output=True, text=True)
+    assert r.returncode != 0 and "written for gfx950" in (r.stderr + r.stdout)

@@ -114,6 +114,67 @@ def test_sharded_ring_and_means_match_single_process(world, N):
         np.testing.assert_allclose(r[5], want_mean, rtol=1e-5, atol=1e-6)  # all_reduce form
 
 
+def _exact_mean_worker(rank, world, port, N, P, orders, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    parallel.init_process_group("gloo", rank=rank, world_size=world, timeout_s=120)
+    try:
+        X = np.random.default_rng(29).standard_normal((N, P)).astype(np.float32)
+        X[3, 5] = -0.0
+        X[N - 1, :3] = [np.inf, -1e-42, 3e38]
+        lo, hi = parallel.shard_bounds(N, world, rank)
+        rows = torch.zeros(max(hi - lo, 1), P + 5)  # ld = P + 5: rows are strided views
+        rows[:hi - lo, :P] = torch.from_numpy(X[lo:hi])
+        outs = [parallel.global_mean_exact(rows, lo, hi, list(o), P, ordered_sum=cpu_ordered_sum)[:P].clone().numpy()
+                for o in orders]
+        q.put((rank, outs))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,N,P", [(2, 10, 37), (3, 11, 200), (8, 35, 1000), (8, 64, 65)])
+def test_exact_mean_all_to_all_matches_reference_order(world, N, P):
+    """parallel.global_mean_exact (one all_to_all of the sampled rows to
+    column blocks, an ordered sum per block, one all_gather) is bit-identical
+    to average_weights' sequential order (DEC/servers.py:42-48) for random
+    full permutations, partial samples, one agent, every sample on one rank,
+    and ranks that own no columns (P = 65 over 8 ranks) or no sampled rows."""
+    rng = np.random.default_rng(31)
+    orders = [rng.permutation(N), rng.choice(N, N // 3, replace=False), np.array([N - 1]),
+              np.arange(N)[::-1], np.array([0, 1, 2]), np.array([N - 1, 0, N // 2, 3, 1])]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_exact_mean_worker, args=(r, world, port, N, P, orders, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    X = np.random.default_rng(29).standard_normal((N, P)).astype(np.float32)
+    X[3, 5] = -0.0
+    X[N - 1, :3] = [np.inf, -1e-42, 3e38]
+    for k, o in enumerate(orders):
+        want = oracle.ordered_mean(X, o)
+        for r in range(world):
+            assert oracle.bits_equal(res[r][k], want), f"order {k}, rank {r}"
+
+
+def test_exact_mean_plan_bookkeeping():
+    """perm maps the k-th sampled agent to its row in the received block
+    (sources in rank order, each source's rows in global order)."""
+    bounds = [(0, 3), (3, 7), (7, 8)]
+    order = [5, 0, 7, 3, 2]
+    mine, counts, perm, cols = parallel.exact_mean_plan(order, bounds, 130, 3, 1)
+    assert mine.tolist() == [2, 0] and counts.tolist() == [2, 2, 1]
+    # received block: rank 0's [0, 2], rank 1's [5, 3], rank 2's [7]
+    assert perm.tolist() == [2, 0, 4, 3, 1]
+    assert cols == [(0, 64), (64, 128), (128, 130)]
+    with pytest.raises(ValueError):
+        parallel.exact_mean_plan([8], bounds, 130, 3, 0)
+
+
 def cpu_apply_csr(csr):
     def apply(X, Y, P=None):
         Y[:, :P] = torch.from_numpy(oracle.mix_csr(X[:, :P].numpy(), csr.rowptr, csr.col, csr.val))
