@@ -60,7 +60,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=4.0, help="CPU seconds per sample below 512 agents")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline (profiling runs)")
     ap.add_argument("--no-copy", action="store_true", help="skip the copy-kernel calibration")
-    ap.add_argument("--map-ring", type=int, default=0, help="1: the ring's x / y as mapped blocks (dol_bank_alloc); 0: torch's allocator")
+    ap.add_argument("--map-ring", type=int, default=1, help="1: the ring's x / y as mapped blocks (dol_bank_alloc, the bank default); 0: torch's allocator")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_ring_8192x1M.json"))
     ap.add_argument("--no-primal-dual", action="store_true", help="skip the secondary measurements (primal/dual round, FedLCon eps=5, dense ER mix)")
     ap.add_argument("--pd-steps", type=int, default=10)
@@ -612,11 +612,9 @@ def main():
     dolhip.lib()
     N, P = args.agents, args.params
     wp, wn = ring_weights(N)
-    # --map-ring 1: the headline's two buffers as mapped physical blocks
-    # (bank.device_matrix).  In one process they ran 2 % faster than hipMalloc'd
-    # ones (profiles/r04e_alloc_probe.jsonl); across processes on one box the
-    # difference drowns in the per-process spread (10.97-11.43 mapped vs
-    # 10.93-11.20 ms, profiles/r04l_map_ab.txt), so the default is torch's allocator
+    # --map-ring 1 (default): the headline's two buffers as mapped physical
+    # blocks, like every bank matrix of >= 1 GiB (bank.device_matrix; in one
+    # process 10.69 vs 10.90 ms for torch-allocated ones, profiles/r05d_alloc_ab.jsonl)
     ring = ShardedRing(N, P, wp, wn, device, mapped=bool(args.map_ring))
     g = torch.Generator(device=device).manual_seed(2028 + rank)
     ring.x.normal_(generator=g)

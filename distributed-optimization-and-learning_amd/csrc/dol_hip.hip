@@ -1541,6 +1541,19 @@ int dol_bank_free(void* ptr, int64_t mapped_bytes) {
       return fail(-static_cast<int>(e), "dol_bank_free: hipMemUnmap: %s", hipGetErrorString(e));
     blk.stage = 1;
   }
+  if (blk.stage == 1 && !env_int("DOL_BANK_FREE_VA", 0)) {
+    // The virtual range stays reserved (retired, never handed out again): on
+    // this ROCm stack a new physical allocation mapped at a range a freed block
+    // used is not what the GPU then reads and writes -- stale translations of
+    // the old block.  tools/vmm_remap_probe.py, 12 map/free cycles in one
+    // process (profiles/r05c_vmm_remap_probe.jsonl): with the range freed and
+    // re-used, 7 of 11 re-mapped cycles returned wrong mix results; with the
+    // range retired, or with nothing freed, all 12 were bit-exact.  A stale
+    // translation to a released range is also the r04k illegal-address fault.
+    // Retiring costs address space only (the physical memory is released).
+    // DOL_BANK_FREE_VA=1 restores the freeing order (diagnostics only).
+    blk.stage = 2;
+  }
   if (blk.stage == 1) {
     if ((e = hipMemAddressFree(ptr, blk.size)) != hipSuccess)
       return fail(-static_cast<int>(e), "dol_bank_free: hipMemAddressFree: %s", hipGetErrorString(e));

@@ -134,19 +134,23 @@ MAPPED_MIN_BYTES = 1 << 30
 
 
 def device_matrix(rows: int, cols: int, device, zero: bool = False, mapped: Optional[bool] = None) -> torch.Tensor:
-    """A [rows, cols] fp32 device matrix for bank state, from torch's caching
-    allocator.  DOL_BANK_ALLOC=vmm (opt-in) makes large ones (>= 1 GiB) ONE
-    mapped physical allocation (dol_bank_alloc: hipMemCreate + hipMemMap): the
-    ring round at 8192 x 2^20 ran 10.93-10.96 ms on such buffers against
-    11.15-11.17 on hipMalloc'd ones, alternating in one process
-    (tools/alloc_probe.hip, profiles/r04e_alloc_probe.jsonl).  Not the
-    default: a process that mapped, freed and re-mapped eleven 4 GiB blocks in
-    a row (tools/bench_configs.py's DGD rounds) once ended in a GPU memory
-    fault (r04, profiles/r04k_vmm_fault.txt), cause not isolated.  mapped=True
-    / False decides for this matrix regardless of the environment (bench.py
-    maps the headline ring's two buffers, allocated once per process)."""
+    """A [rows, cols] fp32 device matrix for bank state.  Matrices of >= 1 GiB
+    are ONE mapped physical allocation (dol_bank_alloc: hipMemCreate +
+    hipMemMap) by default; DOL_BANK_ALLOC=torch (or mapped=False) takes
+    torch's caching allocator instead.  In one process, both pairs held at
+    once and alternated (tools/alloc_ab.py, profiles/r05d_alloc_ab.jsonl), the
+    8192 x 2^20 ring round ran 10.69 ms on mapped buffers against 10.90 on
+    torch-allocated ones, and FedLCon's eps = 5 pass 12.79 against 13.30-13.39.
+    r04 made this opt-in after a GPU memory fault in a process that had mapped
+    and freed many blocks (profiles/r04k_vmm_fault.txt); r05 found the cause:
+    a block mapped at a virtual range a freed block used is read and written
+    through stale translations of the old block (7 of 11 re-mapped cycles
+    wrong, profiles/r05c_vmm_remap_probe.jsonl).  dol_bank_free now retires
+    the range instead of freeing it, and twelve map/free cycles are bit-exact
+    (tests/test_bank_alloc_gpu.py::test_mapped_blocks_survive_map_free_remap_cycles).
+    mapped=True / False decides for this matrix regardless of the environment."""
     device = torch.device(device)
-    want = os.environ.get("DOL_BANK_ALLOC", "torch") == "vmm" if mapped is None else bool(mapped)
+    want = os.environ.get("DOL_BANK_ALLOC", "vmm") == "vmm" if mapped is None else bool(mapped)
     if want and device.type == "cuda" and rows * cols * 4 >= MAPPED_MIN_BYTES:
         t = torch.as_tensor(_MappedBlock(rows, cols, device), device=device)
         if zero:

@@ -21,7 +21,7 @@ def test_headline_stride():
     assert B.row_stride(1 << 20) == (1 << 20) + 2048
 
 
-def test_device_matrix_defaults_to_torch_allocator(monkeypatch):
+def test_device_matrix_never_maps_cpu_matrices(monkeypatch):
     monkeypatch.delenv("DOL_BANK_ALLOC", raising=False)
     made = []
     monkeypatch.setattr(B, "_MappedBlock", lambda *a: made.append(a))
