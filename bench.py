@@ -297,9 +297,30 @@ def primal_dual_round(N: int, P: int, world: int, rank: int, device, steps: int,
         ms = float(np.mean([a.elapsed_time(b) for a, b in ev[nm]]))
         kern[nm] = {"ms": ms, "GBps": alg[nm] / (ms / 1e3) / 1e9, "frac": alg[nm] / (ms / 1e3) / 1e9 / HBM_PEAK_GBPS,
                     "algorithmic_bytes": alg[nm]}
+    exact = None
+    if world > 1:
+        # the bit-exact server mean across ranks (DEC/servers.py:42-48's order):
+        # one all_to_all of the sampled rows to column blocks, an ordered sum per
+        # block, one all_gather (parallel.global_mean_exact); host-timed, max over ranks
+        from dolhip import parallel as par
+        order = [int(g) for g in prob.sample()]
+        out_t = torch.empty_like(prob.theta)
+        par.global_mean_exact(prob.w, prob.lo, prob.hi, order, P, out=out_t)
+        torch.cuda.synchronize(device)
+        dist.barrier()
+        t1 = time.perf_counter()
+        for _ in range(3):
+            par.global_mean_exact(prob.w, prob.lo, prob.hi, order, P, out=out_t)
+        torch.cuda.synchronize(device)
+        dist.barrier()
+        ex = torch.tensor([(time.perf_counter() - t1) / 3], dtype=torch.float64, device=device)
+        dist.all_reduce(ex, op=dist.ReduceOp.MAX)
+        exact = {"ms": float(ex.item()) * 1e3, "sampled": len(order),
+                 "bytes_moved_per_rank": prob.n * P * 4 * (world - 1) // world,
+                 "what": "global_mean_exact: all_to_all of the sampled rows to column blocks + ordered sum + all_gather"}
     hist = prob.history
     out = {"rounds_per_s": steps / el, "ms_per_round": el / steps * 1e3, "agents": N, "params": P,
-           "local_steps": local_steps, "kernels": kern,
+           "local_steps": local_steps, "kernels": kern, "exact_mean": exact,
            "primal_resid_sq_last": hist[-1]["primal_resid_sq"], "dual_sq_last": hist[-1]["dual_sq"],
            "what": "FedADMM least-squares round over all agents: fused client round (w = theta, %d momentum-SGD "
                    "steps with the ADMM term, dual ascent) + all_reduce mean" % local_steps}
@@ -506,8 +527,10 @@ def config5_round_sharded(device, world: int, rank: int, N: int = 1024, reps: in
     el = float(el.item()) / reps
     out = {"agents": N, "params": sim.P, "batch": B, "mlp": f"{d}-{h}-{c}", "ms_per_round": el * 1e3,
            "rounds_per_s": 1.0 / el, "ranks": world, "agents_per_rank": sim.n_local, "columns_per_rank": sim.tr.Pc,
-           "what": "config 5 over ranks (TimeVaryingMLPGossip): fused MLP step on each rank's agents, all_to_all to "
-                   "parameter-column blocks, bit-exact ER mix per block (same W on every rank), all_to_all back"}
+           "overlap_chunks": sim.overlap_chunks,
+           "what": "config 5 over ranks (TimeVaryingMLPGossip): fused MLP step on each rank's agents in pieces, each "
+                   "piece's all_to_all to parameter-column blocks posted while the next piece steps, bit-exact ER mix "
+                   "per block (same W on every rank), all_to_all back"}
     del sim
     torch.cuda.empty_cache()
     return out

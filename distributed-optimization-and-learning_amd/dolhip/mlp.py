@@ -95,18 +95,27 @@ class BatchedMLP:
 
     def step(self, X: torch.Tensor, y: torch.Tensor, lr: float, momentum: float, first_step: bool,
              theta: Optional[torch.Tensor] = None, rho: float = 0.0, admm: bool = False,
-             write_grad: bool = False) -> torch.Tensor:
-        """One fused local iteration for every agent (one kernel launch)."""
+             write_grad: bool = False, rows: Optional[slice] = None,
+             loss: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """One fused local iteration for every agent (one kernel launch), or
+        for the agents `rows` only (a contiguous slice; X / y / loss are then
+        the full [n, ...] tensors and only those rows are read / written).
+        Each agent's step is independent of the others, so stepping the bank
+        slice by slice gives the same bits as one launch."""
         from . import ops
         b = self.bank
-        loss = torch.empty(b.n, dtype=torch.float32, device=b.device)
-        ops.mlp_step(b.buffer("x"), X, y, self.d, self.h, self.c,
-                     grad=b.buffer("grad") if write_grad else None,
-                     mom=b.buffer("mom", zero=True) if momentum != 0.0 else None,
-                     theta=theta, alpha=b.buffer("alpha", zero=True) if admm else None, loss=loss,
-                     lr=lr, momentum=momentum, rho=rho, first_step=first_step, update=True)
+        sl = slice(0, b.n) if rows is None else slice(*rows.indices(b.n)[:2])
+        if loss is None:
+            loss = torch.empty(b.n, dtype=torch.float32, device=b.device)
+        if sl.stop > sl.start:
+            pick = (lambda t: t) if rows is None else (lambda t: t[sl])
+            ops.mlp_step(pick(b.buffer("x")), pick(X), pick(y), self.d, self.h, self.c,
+                         grad=pick(b.buffer("grad")) if write_grad else None,
+                         mom=pick(b.buffer("mom", zero=True)) if momentum != 0.0 else None,
+                         theta=theta, alpha=pick(b.buffer("alpha", zero=True)) if admm else None, loss=pick(loss),
+                         lr=lr, momentum=momentum, rho=rho, first_step=first_step, update=True)
         if momentum != 0.0:
-            b.mark_momentum_started(slice(0, b.n))
+            b.mark_momentum_started(sl)
         return loss
 
     def step_unfused(self, X: torch.Tensor, y: torch.Tensor, lr: float, momentum: float, first_step: bool,

@@ -354,6 +354,8 @@ class AgentColumnTranspose:
         self.direct = self.world > 1 and self.Pc > 0 and self.Pc % 4 == 0
         self._buf_cols2 = (torch.empty(self.N * self.Pc, dtype=torch.float32, device=self.device)
                            if self.direct else None)
+        self._stage = None  # mix_with_local_steps: the pieces' receive staging (allocated on first use)
+        self._side = None
 
     def set_plan(self, plan) -> None:
         if (plan.n_rows, plan.n_cols) != (self.N, self.N):
@@ -421,6 +423,126 @@ class AgentColumnTranspose:
                 raise RuntimeError("AgentColumnTranspose.mix: set_plan() first")
             self.plan.apply(X, Y, P=self.Pc)
 
+    def _chunk_bounds(self, q: int, chunks: int) -> List[Tuple[int, int]]:
+        """Rank q's local rows cut into `chunks` contiguous pieces (some may be empty)."""
+        n_q = self.row_bounds[q][1] - self.row_bounds[q][0]
+        return [shard_bounds(n_q, chunks, c) for c in range(chunks)]
+
+    def mix_with_local_steps(self, rows: torch.Tensor, step_rows, chunks: int = 2,
+                             out: Optional[torch.Tensor] = None, before_mix=None) -> torch.Tensor:
+        """The round's local steps AND its mix, with the first exchange
+        overlapped with the steps: this rank's agent rows
+        are stepped in `chunks` contiguous pieces (step_rows(a, b): the local
+        step of local rows [a, b), enqueued on the current stream); as soon as
+        piece c is enqueued, piece c + 1 is enqueued too, and piece c is packed
+        on a side stream and sent to the column blocks by its own all_to_all
+        (NCCL: on RCCL's stream, behind the pack; the next piece's step runs
+        meanwhile).  The side stream places each received piece at its agents'
+        rows of the [N, Pc] block, the compute stream waits for all of them,
+        and the mix and the way back are those of mix().  Every element is the
+        same computation as step-all-then-mix() (bit-identical): the steps are
+        per agent and the block is the same block.  before_mix(): called on the
+        compute stream right before the mix (e.g. wait for the round's W)."""
+        out = rows if out is None else out
+        if self.world == 1:
+            step_rows(0, self.n_local)
+            if before_mix is not None:
+                before_mix()
+            return self.mix(rows, out)
+        N, P, Pc, n = self.N, self.P, self.Pc, self.n_local
+        dev = self.device
+        main = torch.cuda.current_stream(dev) if dev.type == "cuda" else None
+        side = self._side_stream()
+        mine = self._chunk_bounds(self.rank, chunks)
+        block = self._buf_cols[:N * Pc].view(N, Pc) if Pc > 0 else None
+        if self._stage is None or self._stage.numel() < max(N * Pc, 1):
+            self._stage = torch.empty(max(N * Pc, 1), dtype=torch.float32, device=dev)
+        posted = []
+        stage_off = 0
+        step_rows(*mine[0])
+        for c in range(chunks):
+            a, b = mine[c]
+            ev = None
+            if main is not None:
+                ev = torch.cuda.Event()
+                ev.record(main)
+            if c + 1 < chunks:  # the next piece's step goes in before this piece's exchange
+                step_rows(*mine[c + 1])
+            src = [self._chunk_bounds(s, chunks)[c] for s in range(self.world)]
+            m_src = [hi - lo for lo, hi in src]
+            stage = self._stage[stage_off:stage_off + sum(m_src) * Pc]
+            stage_off += sum(m_src) * Pc
+            with self._on(side):
+                if ev is not None:
+                    side.wait_event(ev)
+                send = self._buf_rows[a * P:b * P]
+                off = 0
+                for qa, qb in self.col_bounds:  # to rank q: my piece's rows x its columns
+                    if b > a and qb > qa:
+                        send[off:off + (b - a) * (qb - qa)].view(b - a, qb - qa).copy_(rows[a:b, qa:qb])
+                    off += (b - a) * (qb - qa)
+                handle = self._post_all_to_all(stage, send, [m * Pc for m in m_src],
+                                               [(b - a) * (qb - qa) for qa, qb in self.col_bounds])
+            posted.append((handle, stage, src))
+        with self._on(side):
+            for handle, stage, src in posted:
+                self._finish_all_to_all(handle, stage)
+                off = 0
+                for s, (lo, hi) in enumerate(src):
+                    if hi > lo and Pc > 0:  # rank s's piece: its agents lo_s + [lo, hi)
+                        g0 = self.row_bounds[s][0]
+                        block[g0 + lo:g0 + hi].copy_(stage[off:off + (hi - lo) * Pc].view(hi - lo, Pc))
+                    off += (hi - lo) * Pc
+        if main is not None:
+            main.wait_stream(side)
+        if before_mix is not None:
+            before_mix()
+        return self._mix_block_and_return(out)
+
+    def _side_stream(self):
+        if self.device.type != "cuda":
+            return None
+        if self._side is None:
+            self._side = torch.cuda.Stream(self.device)
+        return self._side
+
+    @staticmethod
+    def _on(stream):
+        import contextlib
+        return torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
+
+    def _post_all_to_all(self, recv: torch.Tensor, send: torch.Tensor, recv_splits, send_splits):
+        """Start an all_to_all_single on the current stream's data; returns a handle."""
+        if self._staged():
+            hs, hr = send.cpu(), torch.empty(recv.shape, dtype=recv.dtype)
+            return dist.all_to_all_single(hr, hs, recv_splits, send_splits, group=self.group, async_op=True), hr
+        return dist.all_to_all_single(recv, send, recv_splits, send_splits, group=self.group, async_op=True), None
+
+    def _finish_all_to_all(self, handle, recv: torch.Tensor) -> None:
+        work, host = handle
+        if host is not None:
+            _wait_all([work], self.group)
+            recv.copy_(host)
+        else:
+            work.wait()  # the current stream waits for the transfer (RCCL: stream-side)
+
+    def _mix_block_and_return(self, out: torch.Tensor) -> torch.Tensor:
+        """Mix the assembled [N, Pc] block (self._buf_cols) and send it back to the agent rows `out`."""
+        n, N, Pc = self.n_local, self.N, self.Pc
+        if not self.direct:
+            if Pc > 0:
+                self.cols[:, :Pc].copy_(self._buf_cols[:N * Pc].view(N, Pc))
+                self._apply_block(self.cols, self.cols_out)
+            self.from_columns(out)
+            return out
+        Y = self._buf_cols2[:N * Pc]
+        self._apply_block(self._buf_cols[:N * Pc].view(N, Pc), Y.view(N, Pc))
+        back = self._buf_rows[:n * self.P]
+        self._all_to_all(Y, back, [(h - l) * Pc for l, h in self.row_bounds],
+                         [n * (b - a) for a, b in self.col_bounds])
+        self._unpack_rows(back, out)
+        return out
+
     def mix(self, rows: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """One Jacobi round Y = W X for this rank's agents (out may be rows' own
         storage: the column block is a separate buffer)."""
@@ -431,16 +553,9 @@ class AgentColumnTranspose:
             # all_to_all -> unpack: the same elements and the same arithmetic as
             # the staged path below, without its two block copies
             n, N, Pc = self.n_local, self.N, self.Pc
-            recv = self._buf_cols[:N * Pc]
-            self._all_to_all(self._pack_rows(rows), recv, [n * (b - a) for a, b in self.col_bounds],
+            self._all_to_all(self._pack_rows(rows), self._buf_cols[:N * Pc], [n * (b - a) for a, b in self.col_bounds],
                              [(h - l) * Pc for l, h in self.row_bounds])
-            Y = self._buf_cols2[:N * Pc]
-            self._apply_block(recv.view(N, Pc), Y.view(N, Pc))
-            back = self._buf_rows[:n * self.P]
-            self._all_to_all(Y, back, [(h - l) * Pc for l, h in self.row_bounds],
-                             [n * (b - a) for a, b in self.col_bounds])
-            self._unpack_rows(back, out)
-            return out
+            return self._mix_block_and_return(out)
         self.to_columns(rows)
         if self.Pc > 0:
             self._apply_block(self.cols, self.cols_out)

@@ -329,7 +329,7 @@ class TimeVaryingMLPGossip:
 
     def __init__(self, n_agents: int, d: int = 784, h: int = 128, c: int = 10, p_edge: float = 0.1,
                  lr: float = 0.05, momentum: float = 0.5, seed: int = 2028, device=None, group=None,
-                 init_std: float = 0.05):
+                 init_std: float = 0.05, overlap_chunks: int = 2):
         import torch.distributed as dist
         from . import parallel
         from .mlp import BatchedMLP, mlp_layout
@@ -352,6 +352,7 @@ class TimeVaryingMLPGossip:
         if self.mu != 0.0:
             self.bank.buffer("mom", zero=True)
         self.tr = parallel.AgentColumnTranspose(self.N, self.P, self.device, group) if self.world > 1 else None
+        self.overlap_chunks = max(1, int(overlap_chunks))  # pieces of the local step overlapped with the exchange
         self._W = torch.empty(self.N, self.N, device=self.device)
         self._plan = None
         self._side = torch.cuda.Stream(self.device)
@@ -378,21 +379,36 @@ class TimeVaryingMLPGossip:
             W = G.erdos_renyi_stochastic_hip(self.N, self.p_edge, self.round_seed(self.rounds), self.device,
                                              out=self._W)
             self._plan = G.MixingPlan.from_dense(W, dense_kernel="csr", reuse=self._plan)
-        loss = self.mlp.step(self.X, self.y, lr=self.lr, momentum=self.mu, first_step=(self.rounds == 0))
+        if self.tr is None:
+            loss = self.mlp.step(self.X, self.y, lr=self.lr, momentum=self.mu, first_step=(self.rounds == 0))
+            self._plan_ready(main)
+            self.bank.mix(self._plan)
+        else:
+            # the local steps in pieces, each piece's first exchange posted while
+            # the next piece steps (parallel.AgentColumnTranspose.mix_with_local_steps)
+            loss = torch.empty(self.n_local, dtype=torch.float32, device=self.device)
+
+            def step_rows(a, b):
+                self.mlp.step(self.X, self.y, lr=self.lr, momentum=self.mu, first_step=(self.rounds == 0),
+                              rows=slice(a, b), loss=loss)
+
+            def before_mix():
+                self._plan_ready(main)
+                self.tr.set_plan(self._plan)
+            self.tr.mix_with_local_steps(self.bank.rows(), step_rows, chunks=self.overlap_chunks,
+                                         before_mix=before_mix)
+        self.rounds += 1
+        self.last_loss = loss
+        return loss
+
+    def _plan_ready(self, main) -> None:
+        """The compute stream waits for the side stream's W draw + plan build."""
         main.wait_stream(self._side)
         # the plan's buffers were allocated on the side stream and are read on the
         # main one: tell the caching allocator, so freeing them never races the mix
         for t in (self._plan.rowptr, self._plan.col, self._plan.val, self._plan.ent, self._plan.hdr):
             if t is not None:
                 t.record_stream(main)
-        if self.tr is None:
-            self.bank.mix(self._plan)
-        else:
-            self.tr.set_plan(self._plan)
-            self.tr.mix(self.bank.rows())
-        self.rounds += 1
-        self.last_loss = loss
-        return loss
 
     def params(self) -> torch.Tensor:
         return self.bank.rows()

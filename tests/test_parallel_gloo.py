@@ -348,7 +348,7 @@ def test_column_sharded_set_plan_keeps_injected_entries():
     assert calls == ["checker", "checker", "b-dgd", "dgd-checker", "checker"]
 
 
-def _transpose_worker(rank, world, port, N, P, rounds, q):
+def _transpose_worker(rank, world, port, N, P, rounds, q, chunks=0):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     parallel.init_process_group("gloo", rank=rank, world_size=world, timeout_s=120)
@@ -360,8 +360,11 @@ def _transpose_worker(rank, world, port, N, P, rounds, q):
         for k in range(rounds):  # a new W every round (config 5), the same on every rank
             csr = _er_csr(N, 0.3, seed=100 + k)
             tr._apply = cpu_apply_csr(csr)
-            rows.mul_(0.5).add_(0.25)  # a stand-in local step on the agent-major block
-            tr.mix(rows)
+            if chunks:  # the local step in pieces, each piece's exchange posted behind it
+                tr.mix_with_local_steps(rows, lambda a, b: rows[a:b].mul_(0.5).add_(0.25), chunks=chunks)
+            else:
+                rows.mul_(0.5).add_(0.25)  # a stand-in local step on the agent-major block
+                tr.mix(rows)
         q.put((rank, tr.lo, rows.numpy().copy()))
     finally:
         dist.destroy_process_group()
@@ -378,17 +381,21 @@ def _er_csr(n, p, seed):
     return G.csr_from_dense(W)
 
 
+@pytest.mark.parametrize("chunks", [0, 2, 3])
 @pytest.mark.parametrize("world,N,P", [(2, 30, 300), (3, 25, 130), (4, 9, 70)])
-def test_agent_column_transpose_mix_matches_single_process(world, N, P):
+def test_agent_column_transpose_mix_matches_single_process(world, N, P, chunks):
     """Config 5 across ranks (parallel.AgentColumnTranspose): agent-major blocks
     for the local step, one all_to_all to parameter-column blocks, the mix with a
     new W per round on every block, one all_to_all back -- bit-identical to one
-    process (uneven agent and column blocks, a rank with no columns at P = 70)."""
+    process (uneven agent and column blocks, a rank with no columns at P = 70).
+    chunks > 0: mix_with_local_steps, the step in pieces whose first exchange
+    is posted piece by piece (empty pieces at N = 9 over 4 ranks)."""
     rounds = 3
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_transpose_worker, args=(r, world, port, N, P, rounds, q)) for r in range(world)]
+    procs = [ctx.Process(target=_transpose_worker, args=(r, world, port, N, P, rounds, q, chunks))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = sorted(q.get(timeout=120) for _ in range(world))

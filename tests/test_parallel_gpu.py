@@ -354,7 +354,7 @@ def test_sharded_admm_real_kernels_on_one_gpu(world, mean, gpu):
             np.testing.assert_allclose(r[4], th, rtol=1e-5, atol=1e-6)
 
 
-def _config5_worker(rank, world, port, N, rounds, q):
+def _config5_worker(rank, world, port, N, rounds, q, chunks=2):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, os.path.join(root, "distributed-optimization-and-learning_amd"))
@@ -363,7 +363,7 @@ def _config5_worker(rank, world, port, N, rounds, q):
     os.environ["MASTER_PORT"] = str(port)
     parallel.init_process_group("gloo", rank=rank, world_size=world, timeout_s=120)
     try:
-        q.put((rank, _config5_sim(N, rounds, torch.device("cuda:0"))))
+        q.put((rank, _config5_sim(N, rounds, torch.device("cuda:0"), chunks)))
     finally:
         dist.destroy_process_group()
 
@@ -377,10 +377,11 @@ def _config5_batch(N, dev):
             torch.randint(0, _C5[2], (N, 8), device=dev, generator=g))
 
 
-def _config5_sim(N, rounds, dev):
+def _config5_sim(N, rounds, dev, chunks=2):
     """dolhip.synthetic.TimeVaryingMLPGossip for `rounds` rounds on this rank."""
     from dolhip.synthetic import TimeVaryingMLPGossip
-    sim = TimeVaryingMLPGossip(N, *_C5, p_edge=0.1, lr=0.05, momentum=0.5, seed=31, device=dev)
+    sim = TimeVaryingMLPGossip(N, *_C5, p_edge=0.1, lr=0.05, momentum=0.5, seed=31, device=dev,
+                               overlap_chunks=chunks)
     Xb, yb = _config5_batch(N, dev)
     sim.batch(Xb[sim.lo:sim.hi].contiguous(), yb[sim.lo:sim.hi].contiguous())
     for _ in range(rounds):
@@ -412,13 +413,16 @@ def _config5_by_hand(N, rounds, dev):
     return bank.rows().cpu().numpy()
 
 
-@pytest.mark.parametrize("world,N", [(1, 70), (2, 70), (3, 130)])
-def test_config5_rounds_across_ranks_match_one_gpu(world, N, gpu):
+@pytest.mark.parametrize("world,N,chunks", [(1, 70, 2), (2, 70, 2), (3, 130, 2), (2, 70, 1), (3, 130, 3)])
+def test_config5_rounds_across_ranks_match_one_gpu(world, N, chunks, gpu):
     """BASELINE config 5 (dolhip.synthetic.TimeVaryingMLPGossip): the fused MLP
     local step on each rank's agent block, a new Erdos-Renyi W per round (device
     draw + device Neighbors on a side stream, the same on every rank), the exact
     mix on parameter-column blocks between two all_to_alls -- bit-identical to
-    the rounds assembled by hand on one GPU (DIST/clients.py:34-69)."""
+    the rounds assembled by hand on one GPU (DIST/clients.py:34-69).  Across
+    ranks the local step runs in `chunks` pieces, each piece's first exchange
+    posted from a side stream while the next piece steps
+    (AgentColumnTranspose.mix_with_local_steps)."""
     import oracle
     rounds = 3
     want = _config5_by_hand(N, rounds, gpu)
@@ -428,7 +432,8 @@ def test_config5_rounds_across_ranks_match_one_gpu(world, N, gpu):
         ctx = mp.get_context("spawn")
         q = ctx.Queue()
         port = _free_port()
-        procs = [ctx.Process(target=_config5_worker, args=(r, world, port, N, rounds, q)) for r in range(world)]
+        procs = [ctx.Process(target=_config5_worker, args=(r, world, port, N, rounds, q, chunks))
+                 for r in range(world)]
         for p in procs:
             p.start()
         res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda t: t[0])
