@@ -123,6 +123,10 @@ class ShardedRing:
         self.w_next = wn[self.lo:self.hi].contiguous().to(self.device)
         self.prev_rank = (self.rank - 1) % self.world
         self.next_rank = (self.rank + 1) % self.world
+        if mapped is None and self.world > 1:
+            # the boundary rows are handed to RCCL send/recv as they are: across
+            # ranks keep them on torch's allocator (the memory RCCL users pass)
+            mapped = False
         if alloc:
             self.x = device_matrix(self.n_local, self.ld, self.device, mapped=mapped)
             self.y = device_matrix(self.n_local, self.ld, self.device, mapped=mapped)
