@@ -428,6 +428,146 @@ void dense_split3_kernel(const uint8_t* __restrict__ WA, const uint8_t* __restri
     }
 }
 
+// FX8 (r05): the in-register X split without redundancy, so the GEMM needs no
+// X split pass (at 1024 x 101,770 the pass moved 1.04 GB in 0.18 ms of a
+// 1.03 ms round).  Each of the tile's CB waves owns 32 output columns and ALL
+// 256 rows (8 row blocks of 32): per k-step it reads its own 32 columns' 16 X
+// values from the fp32 stage (8 per lane), splits them once (split8: the
+// split pass's bits), then runs the six MFMAs of each of its 8 row blocks,
+// reading the A records (the split W) block by block.  The r01 FX kernel's
+// 2 x 2 waves split every B value twice and four column blocks per wave
+// (~250 VALU per stage and wave); here it is 8 values per lane.  Each output
+// element sees the same k-steps and the same six MFMAs in the same order as
+// dense_split3_kernel: bit-identical.  CB = 8: 256 x 256 tiles, 8 waves (two
+// per SIMD); CB = 2: 256 x 64 quarter tiles for the last, partial wave of
+// tiles.  Stage: A records (24 KiB) + 16 fp32 X rows of CB * 32 columns
+// (pitch 1040 B at CB = 8: the two lane halves read rows 8 apart on different
+// banks; 256 B at CB = 2).
+template <int CB>
+struct Fx8Geom {
+  static constexpr int kCols = 32 * CB;
+  static constexpr int kRowBytes = 4 * kCols;                       // one fp32 X row of the tile
+  static constexpr int kPitch = CB == 8 ? kRowBytes + 16 : kRowBytes;
+  static constexpr int kStage = kOpStage + 16 * kPitch;
+  static constexpr int kRowsPerDma = 1024 / kRowBytes;              // rows per 1-KiB DMA instruction
+  static constexpr int kDmaTot = 24 + 16 / kRowsPerDma;             // A pieces + B pieces per stage
+  static constexpr int kDma = kDmaTot / CB;                         // per wave
+  static_assert(kDmaTot % CB == 0, "DMA pieces must split evenly over the waves");
+  static_assert(CB == 8 || kPitch == kRowBytes, "multi-row DMA pieces need contiguous rows");
+};
+
+template <int CB>
+__global__ __launch_bounds__(64 * CB) __attribute__((amdgpu_waves_per_eu(CB == 8 ? 2 : 1, CB == 8 ? 2 : 1)))
+void dense_split3_fx8_kernel(const uint8_t* __restrict__ WA, float* __restrict__ Y, int64_t ldy, int M, int64_t P,
+                             int64_t Mp, int n_stages, int n_mt, int64_t n_pt, int64_t tiles_per_xcd, int group_m,
+                             const float* __restrict__ X, int64_t ldx, int K, int64_t pread, int64_t t_base,
+                             int64_t t_end) {
+  using Gm = Fx8Geom<CB>;
+  constexpr int kParts = 8 / CB;  // narrow tiles per 256-wide tile
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  int64_t t;
+  int part = 0;
+  if constexpr (kParts == 1) {
+    const int64_t j = blockIdx.x >> 3;
+    t = (blockIdx.x & 7) * tiles_per_xcd + j;
+    if (j >= tiles_per_xcd || t >= t_end) return;
+  } else {
+    t = t_base + blockIdx.x / kParts;
+    part = blockIdx.x % kParts;
+    if (t >= t_end) return;
+  }
+  const int64_t per_group = int64_t(group_m) * n_pt;
+  const int g = int(t / per_group);
+  const int first_m = g * group_m;
+  const int gs = min(n_mt - first_m, group_m);
+  const int64_t r = t - int64_t(g) * per_group;
+  const int mt = first_m + int(r % gs);
+  const int64_t pt = r / gs;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int h = lane >> 5, li = lane & 31;
+  const uint8_t* srcA = WA + int64_t(mt) * kTile * kRec + lane * 16;
+  const int64_t pitchA = Mp * kRec;
+  const int64_t col0 = pt * kTile + part * Gm::kCols;  // first P column of the tile
+  // this lane's B DMA source column (16 B of a row; past P: clamped, masked after the read)
+  int64_t cdma = col0 + 4 * (lane % (64 / Gm::kRowsPerDma));
+  if (cdma + 4 > pread) cdma = pread - 4;
+  const int drow = lane / (64 / Gm::kRowsPerDma);  // row within a multi-row B piece
+
+  auto issue = [&](int s) {
+    uint8_t* st = lds + (s % kStages) * Gm::kStage;
+#pragma unroll
+    for (int i = 0; i < Gm::kDma; ++i) {
+      const int q = wave + CB * i;
+      if (q < 24) {  // A: k-group 2s + q / 12, 1-KiB piece q % 12 of the 256 rows' records
+        const uint8_t* src = srcA + (2 * int64_t(s) + q / 12) * pitchA + (q % 12) * 1024;
+        __builtin_amdgcn_global_load_lds(DOL_GPTR(src), DOL_LPTR(st + q * 1024), 16, 0, 0);
+      } else {  // B: X rows 16 s + (q - 24) * kRowsPerDma + drow (rows past K: clamped, masked after the read)
+        const int kr = (q - 24) * Gm::kRowsPerDma;
+        const int k = min(16 * s + kr + drow, K - 1);
+        __builtin_amdgcn_global_load_lds(DOL_GPTR(X + int64_t(k) * ldx + cdma), DOL_LPTR(st + kOpStage + kr * Gm::kPitch),
+                                         16, 0, 0);
+      }
+    }
+  };
+
+  f32x16 acc[8];
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[a][e] = 0.f;
+  const int mycol = 32 * wave + li;  // within the tile
+  const bool col_ok = col0 + mycol < P;
+
+  issue(0);
+  if (n_stages > 1) issue(1);
+  for (int s = 0; s < n_stages; ++s) {
+    wait_vmcnt_le<Gm::kDma>(s + 1 < n_stages);  // my DMA of stage s landed
+    __builtin_amdgcn_s_barrier();               // ... and every wave's; stage (s + 2) % 3 is free
+    asm volatile("" ::: "memory");
+    if (s + 2 < n_stages) issue(s + 2);
+    const uint8_t* st = lds + (s % kStages) * Gm::kStage;
+    // B: this lane's column, k = 16 s + 8 h + j
+    const float* bs = reinterpret_cast<const float*>(st + kOpStage + 8 * h * Gm::kPitch) + mycol;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = bs[j * (Gm::kPitch / 4)];
+    if (!col_ok || 16 * s + 16 > K) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (col_ok && 16 * s + 8 * h + j < K) ? v[j] : 0.f;
+    }
+    bf16x8 fb[3];
+    split8(v, fb[0], fb[1], fb[2]);
+    const uint8_t* sa = st + h * (kTile * kRec) + li * kRec;
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int a = 0; a < 8; ++a) {
+      bf16x8 fa[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) fa[p] = *reinterpret_cast<const bf16x8*>(sa + a * 32 * kRec + 16 * p);
+      f32x16 c = acc[a];  // the six piece products of one 32x32x16 block, smallest first (as dense_split3_kernel)
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2], fb[0], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[2], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[1], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[0], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[1], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[0], c, 0, 0, 0);
+      acc[a] = c;
+    }
+    __builtin_amdgcn_s_setprio(0);
+  }
+  // C/D map (gfx950): col = lane & 31, row = (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5)
+  const int64_t col = col0 + mycol;
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int row = mt * kTile + a * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+      if (row < M && col < P) __builtin_nontemporal_store(acc[a][e], Y + int64_t(row) * ldy + col);
+    }
+}
+
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 struct Split3Geom {
@@ -536,7 +676,11 @@ extern "C" int dol_mix_dense_split3_f32(const float* W, int64_t ldw, const float
   const char* cus_env = getenv("DOL_SPLIT3_CUS");
   const int64_t cus = cus_env && *cus_env ? atoi(cus_env) : n_cu;
   const int64_t tail = cus > 0 ? n_tiles % cus : 0;
-  const bool narrow_tail = !fx && probe == 0 && n_tiles > cus && tail > 0 && 2 * tail <= cus;
+  // FUSE_X runs dense_split3_fx8_kernel (r05) unless DOL_SPLIT3_FX=1 asks for the r01 in-register kernel
+  static const bool fx_old = [] { const char* e = getenv("DOL_SPLIT3_FX"); return e && atoi(e) == 1; }();
+  const bool fx8 = fx && !fx_old && probe == 0;
+  const bool fx8_tail = fx8 && n_tiles > cus && tail > 0 && 4 * tail <= cus;  // 256 x 64 quarters, one CU each
+  const bool narrow_tail = (!fx && probe == 0 && n_tiles > cus && tail > 0 && 2 * tail <= cus) || fx8_tail;
   const int nb_tail = 4 * tail <= cus ? 1 : 2;
   const int64_t t_main = narrow_tail ? n_tiles - tail : n_tiles;
   const int64_t tiles_per_xcd = cdiv(t_main, 8);
@@ -551,6 +695,17 @@ extern "C" int dol_mix_dense_split3_f32(const float* W, int64_t ldw, const float
                        pread, t_base, t_end);
   };
   const int64_t grid = 8 * tiles_per_xcd;
+  if (fx8) {
+    auto launch8 = [&](auto kern, int lds, int64_t grd, int64_t t_base, int64_t t_end, int threads) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(grd)), dim3(threads), lds, s, wa, Y, ldy, M, P, g.Mp,
+                         static_cast<int>(g.Kg / 2), n_mt, n_pt, tiles_per_xcd, group_m, X, ldx, K, pread, t_base,
+                         t_end);
+    };
+    launch8(dense_split3_fx8_kernel<8>, kStages * Fx8Geom<8>::kStage, grid, 0, t_main, 512);
+    if (fx8_tail) launch8(dense_split3_fx8_kernel<2>, kStages * Fx8Geom<2>::kStage, 4 * tail, t_main, n_tiles, 128);
+    return dol::check_launch("dol_mix_dense_split3_f32");
+  }
   if (fx) {
     if (probe == 1) launch(dense_split3_kernel<1, true>, kStages * kStageFX, grid, 0, t_main);
     else if (probe == 2) launch(dense_split3_kernel<2, true>, kStages * kStageFX, grid, 0, t_main);

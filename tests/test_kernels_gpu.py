@@ -498,6 +498,33 @@ def test_mix_dense_split3_fused_x_equals_split_pass(M, K, P, extra, gpu):
     assert np.all(err <= _split3_bound(W[ok], X) + 1e-30)
 
 
+@pytest.mark.parametrize("M,K,P,cus", [(300, 300, 2148, 16), (513, 64, 3001, 32), (256, 777, 5137, 0),
+                                       (1024, 1024, 101770, None)])
+def test_mix_dense_split3_fx8_tiles_and_tail_bit_identical(M, K, P, cus, gpu, monkeypatch):
+    """dense_split3_fx8_kernel (r05, the fused X split: each wave splits its own
+    32 columns once and runs 8 row blocks) on 256 x 256 tiles and, for the last
+    partial wave of tiles, 256 x 64 quarters (DOL_SPLIT3_CUS pretends a CU
+    count so small shapes take that path; None: the device's own, 1592 tiles at
+    the bench's 1024 x 101,770): the same bits as the split pass + the
+    record-staged GEMM, padding past P untouched."""
+    rng = np.random.default_rng(M + 3 * K + P)
+    W = ((rng.random((M, K)) < 0.2) * rng.random((M, K))).astype(np.float32)
+    X = rng.standard_normal((K, P)).astype(np.float32)
+    extra = (-P) % 4 + 4  # rows readable up to round_up(P, 4): the fused path
+    Wd, Xd = dev(W, gpu), padded(X, gpu, extra)
+    assert ops.split3_x_flags(Xd, P) != 0
+    Y1, Y2 = padded(np.zeros((M, P), np.float32), gpu, 3), padded(np.zeros((M, P), np.float32), gpu, 3)
+    if cus is None:
+        monkeypatch.delenv("DOL_SPLIT3_CUS", raising=False)
+    else:
+        monkeypatch.setenv("DOL_SPLIT3_CUS", str(cus))
+    ops.mix_dense_split3(Wd, Xd, Y1, P=P, fuse=True)
+    ops.mix_dense_split3(Wd, Xd, Y2, P=P)
+    torch.cuda.synchronize()
+    assert bits_equal(Y1[:, :P].cpu().numpy(), Y2[:, :P].cpu().numpy())
+    assert np.isnan(Y1[:, P:].cpu().numpy()).all()
+
+
 def _er_hip_numpy(n, p, seed):
     """numpy restatement of graph_draw.hip (hash, keys, G = R o A, W = (G / colsum)^T)."""
     M64 = (1 << 64) - 1
