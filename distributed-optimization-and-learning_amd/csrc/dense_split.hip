@@ -431,39 +431,46 @@ void dense_split3_kernel(const uint8_t* __restrict__ WA, const uint8_t* __restri
 // FX8 (r05): the in-register X split without redundancy, so the GEMM needs no
 // X split pass (at 1024 x 101,770 the pass moved 1.04 GB in 0.18 ms of a
 // 1.03 ms round).  Each of the tile's CB waves owns 32 output columns and ALL
-// 256 rows (8 row blocks of 32): per k-step it reads its own 32 columns' 16 X
-// values from the fp32 stage (8 per lane), splits them once (split8: the
-// split pass's bits), then runs the six MFMAs of each of its 8 row blocks,
-// reading the A records (the split W) block by block.  The r01 FX kernel's
-// 2 x 2 waves split every B value twice and four column blocks per wave
-// (~250 VALU per stage and wave); here it is 8 values per lane.  Each output
-// element sees the same k-steps and the same six MFMAs in the same order as
-// dense_split3_kernel: bit-identical.  CB = 8: 256 x 256 tiles, 8 waves (two
-// per SIMD); CB = 2: 256 x 64 quarter tiles for the last, partial wave of
-// tiles.  Stage: A records (24 KiB) + 16 fp32 X rows of CB * 32 columns
-// (pitch 1040 B at CB = 8: the two lane halves read rows 8 apart on different
-// banks; 256 B at CB = 2).
-template <int CB>
+// 256 rows (8 row blocks of 32).  Per k-step a wave
+//   * stages ITS OWN 32 columns of the 16 X rows by LDS-DMA (2 KiB, two 1-KiB
+//     pieces: 8 rows x 128 B each) -- only its own covering vmcnt orders its
+//     reads of them, no barrier -- and the A records (the split W) with the
+//     other waves (24 KiB per stage, behind the workgroup barrier);
+//   * splits its 8 values per lane of the NEXT k-step (split8: the split
+//     pass's bits) while this step's MFMAs run, so the split is off the MFMA
+//     path (a first build split at the top of each step, behind the barrier:
+//     both waves of a SIMD waited on the reads and the split together, 1.011
+//     vs 1.045 ms for the split pass + record GEMM, profiles/r05h_split3_ab.jsonl);
+//   * runs its 8 row blocks' six MFMAs, A fragments read block by block.
+// The r01 FX kernel's 2 x 2 waves split every B value twice and four column
+// blocks per wave.  Each output element sees the same k-steps and the same
+// six MFMAs in the same order as dense_split3_kernel: bit-identical.
+// RW x CW waves, wave (wm, wn) = rows [256 / RW * wm, + 256 / RW) x 32 columns
+// at 32 wn: <1, 8> = 256 x 256 tiles, 8 waves (two per SIMD); <4, 2> = the
+// 256 x 64 quarter tiles of the last, partial wave of tiles, also 8 waves
+// (the four row-waves of a column each stage and split their own copy of
+// its X slice, so no wave waits on another's B).
+template <int RW, int CW>
 struct Fx8Geom {
-  static constexpr int kCols = 32 * CB;
-  static constexpr int kRowBytes = 4 * kCols;                       // one fp32 X row of the tile
-  static constexpr int kPitch = CB == 8 ? kRowBytes + 16 : kRowBytes;
-  static constexpr int kStage = kOpStage + 16 * kPitch;
-  static constexpr int kRowsPerDma = 1024 / kRowBytes;              // rows per 1-KiB DMA instruction
-  static constexpr int kDmaTot = 24 + 16 / kRowsPerDma;             // A pieces + B pieces per stage
-  static constexpr int kDma = kDmaTot / CB;                         // per wave
-  static_assert(kDmaTot % CB == 0, "DMA pieces must split evenly over the waves");
-  static_assert(CB == 8 || kPitch == kRowBytes, "multi-row DMA pieces need contiguous rows");
+  static constexpr int kWaves = RW * CW;
+  static constexpr int kRB = 8 / RW;                       // 32-row blocks per wave
+  static constexpr int kCols = 32 * CW;                    // tile width
+  static constexpr int kBWave = 16 * 128;                  // one wave's X slice per stage: 16 rows x 32 floats
+  static constexpr int kStage = kOpStage + kWaves * kBWave;
+  static constexpr int kDmaA = 24 / kWaves;                // A pieces per wave per stage
+  static constexpr int kDma = kDmaA + 2;                   // + the wave's two B pieces
+  static_assert(24 % kWaves == 0 && 8 % RW == 0, "A pieces / row blocks must split evenly over the waves");
 };
 
-template <int CB>
-__global__ __launch_bounds__(64 * CB) __attribute__((amdgpu_waves_per_eu(CB == 8 ? 2 : 1, CB == 8 ? 2 : 1)))
+template <int RW, int CW, int BATCH = 1>
+__global__ __launch_bounds__(64 * RW * CW)
+__attribute__((amdgpu_waves_per_eu(RW * CW >= 8 ? RW * CW / 4 : 1, RW * CW >= 8 ? RW * CW / 4 : 1)))
 void dense_split3_fx8_kernel(const uint8_t* __restrict__ WA, float* __restrict__ Y, int64_t ldy, int M, int64_t P,
                              int64_t Mp, int n_stages, int n_mt, int64_t n_pt, int64_t tiles_per_xcd, int group_m,
                              const float* __restrict__ X, int64_t ldx, int K, int64_t pread, int64_t t_base,
                              int64_t t_end) {
-  using Gm = Fx8Geom<CB>;
-  constexpr int kParts = 8 / CB;  // narrow tiles per 256-wide tile
+  using Gm = Fx8Geom<RW, CW>;
+  constexpr int kParts = 8 / CW;  // narrow tiles per 256-wide tile
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   int64_t t;
   int part = 0;
@@ -486,66 +493,104 @@ void dense_split3_fx8_kernel(const uint8_t* __restrict__ WA, float* __restrict__
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave / CW, wn = wave % CW;
   const int h = lane >> 5, li = lane & 31;
   const uint8_t* srcA = WA + int64_t(mt) * kTile * kRec + lane * 16;
   const int64_t pitchA = Mp * kRec;
-  const int64_t col0 = pt * kTile + part * Gm::kCols;  // first P column of the tile
-  // this lane's B DMA source column (16 B of a row; past P: clamped, masked after the read)
-  int64_t cdma = col0 + 4 * (lane % (64 / Gm::kRowsPerDma));
+  const int64_t col0 = pt * kTile + part * Gm::kCols + 32 * wn;  // this wave's first P column
+  // B DMA: lane -> row (lane >> 3) of 8, 16 B at column 4 (lane & 7); past P: clamped, masked after the read
+  int64_t cdma = col0 + 4 * (lane & 7);
   if (cdma + 4 > pread) cdma = pread - 4;
-  const int drow = lane / (64 / Gm::kRowsPerDma);  // row within a multi-row B piece
+  const int drow = lane >> 3;
+  uint8_t* const bwave = lds + kOpStage + wave * Gm::kBWave;  // + stage offset
 
   auto issue = [&](int s) {
     uint8_t* st = lds + (s % kStages) * Gm::kStage;
 #pragma unroll
-    for (int i = 0; i < Gm::kDma; ++i) {
-      const int q = wave + CB * i;
-      if (q < 24) {  // A: k-group 2s + q / 12, 1-KiB piece q % 12 of the 256 rows' records
-        const uint8_t* src = srcA + (2 * int64_t(s) + q / 12) * pitchA + (q % 12) * 1024;
-        __builtin_amdgcn_global_load_lds(DOL_GPTR(src), DOL_LPTR(st + q * 1024), 16, 0, 0);
-      } else {  // B: X rows 16 s + (q - 24) * kRowsPerDma + drow (rows past K: clamped, masked after the read)
-        const int kr = (q - 24) * Gm::kRowsPerDma;
-        const int k = min(16 * s + kr + drow, K - 1);
-        __builtin_amdgcn_global_load_lds(DOL_GPTR(X + int64_t(k) * ldx + cdma), DOL_LPTR(st + kOpStage + kr * Gm::kPitch),
-                                         16, 0, 0);
-      }
+    for (int i = 0; i < 2; ++i) {  // B first: a wave's wait for its B slice leaves its A pieces in flight
+      const int k = min(16 * s + 8 * i + drow, K - 1);  // rows past K: clamped, masked after the read
+      __builtin_amdgcn_global_load_lds(DOL_GPTR(X + int64_t(k) * ldx + cdma),
+                                       DOL_LPTR(bwave + (s % kStages) * Gm::kStage + i * 1024), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < Gm::kDmaA; ++i) {  // A: k-group 2s + q / 12, 1-KiB piece q % 12 of the 256 rows' records
+      const int q = wave + Gm::kWaves * i;
+      const uint8_t* src = srcA + (2 * int64_t(s) + q / 12) * pitchA + (q % 12) * 1024;
+      __builtin_amdgcn_global_load_lds(DOL_GPTR(src), DOL_LPTR(st + q * 1024), 16, 0, 0);
     }
   };
-
-  f32x16 acc[8];
+  const bool col_ok = col0 + li < P;
+  // the B fragments of step s from this wave's slice (k = 16 s + 8 h + j of column li)
+  auto read_b = [&](int s, float (&v)[8]) {
+    const float* bs = reinterpret_cast<const float*>(bwave + (s % kStages) * Gm::kStage + 8 * h * 128) + li;
 #pragma unroll
-  for (int a = 0; a < 8; ++a)
-#pragma unroll
-    for (int e = 0; e < 16; ++e) acc[a][e] = 0.f;
-  const int mycol = 32 * wave + li;  // within the tile
-  const bool col_ok = col0 + mycol < P;
-
-  issue(0);
-  if (n_stages > 1) issue(1);
-  for (int s = 0; s < n_stages; ++s) {
-    wait_vmcnt_le<Gm::kDma>(s + 1 < n_stages);  // my DMA of stage s landed
-    __builtin_amdgcn_s_barrier();               // ... and every wave's; stage (s + 2) % 3 is free
-    asm volatile("" ::: "memory");
-    if (s + 2 < n_stages) issue(s + 2);
-    const uint8_t* st = lds + (s % kStages) * Gm::kStage;
-    // B: this lane's column, k = 16 s + 8 h + j
-    const float* bs = reinterpret_cast<const float*>(st + kOpStage + 8 * h * Gm::kPitch) + mycol;
-    float v[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = bs[j * (Gm::kPitch / 4)];
+    for (int j = 0; j < 8; ++j) v[j] = bs[j * 32];
+  };
+  auto split_b = [&](int s, float (&v)[8], bf16x8 (&fb)[3]) {
     if (!col_ok || 16 * s + 16 > K) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = (col_ok && 16 * s + 8 * h + j < K) ? v[j] : 0.f;
     }
-    bf16x8 fb[3];
     split8(v, fb[0], fb[1], fb[2]);
-    const uint8_t* sa = st + h * (kTile * kRec) + li * kRec;
+  };
+
+  f32x16 acc[Gm::kRB];
+#pragma unroll
+  for (int a = 0; a < Gm::kRB; ++a)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[a][e] = 0.f;
+
+  issue(0);
+  if (n_stages > 1) issue(1);
+  bf16x8 fb[3];
+  // my B slice of step 0 landed (step 0's A pieces and step 1 may still fly)
+  if (n_stages > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(Gm::kDmaA + Gm::kDma) : "memory");
+  else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(Gm::kDmaA) : "memory");
+  {
+    float v0[8];
+    read_b(0, v0);
+    split_b(0, v0, fb);
+  }
+  for (int s = 0; s < n_stages; ++s) {
+    wait_vmcnt_le<Gm::kDma>(s + 1 < n_stages);  // my DMA of step s landed
+    __builtin_amdgcn_s_barrier();               // ... and every wave's A pieces; stage (s + 2) % 3 is free
+    asm volatile("" ::: "memory");
+    if (s + 2 < n_stages) issue(s + 2);
+    const uint8_t* sa = lds + (s % kStages) * Gm::kStage + h * (kTile * kRec) + (wm * 32 * Gm::kRB + li) * kRec;
+    bf16x8 fn[3];
+    float vn[8];  // the next step's X values: read now, split under this step's MFMAs
+    if (s + 1 < n_stages) {
+      // my B slice of step s + 1 landed: its A pieces and (if issued) step s + 2 may still fly
+      if (s + 2 < n_stages) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(Gm::kDmaA + Gm::kDma) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(Gm::kDmaA) : "memory");
+      read_b(s + 1, vn);
+    }
+    __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
+    // A fragments: BATCH = 1 double-buffers single blocks (block a + 1's reads
+    // in flight while block a's MFMAs issue); BATCH > 1 reads BATCH blocks'
+    // fragments at once and then runs their MFMAs (one LDS wait per batch).
+    // The scheduler otherwise sinks each read to its use and waits
+    // lgkmcnt(0) before every block's six MFMAs: sched_barrier keeps the
+    // reads where they are written.
+    constexpr int NQ = BATCH == 1 ? 2 : BATCH;
+    bf16x8 fq[NQ][3];
+    auto read_block = [&](int a, bf16x8 (&f)[3]) {
 #pragma unroll
-    for (int a = 0; a < 8; ++a) {
-      bf16x8 fa[3];
+      for (int p = 0; p < 3; ++p) f[p] = *reinterpret_cast<const bf16x8*>(sa + a * 32 * kRec + 16 * p);
+    };
+    if constexpr (BATCH == 1) read_block(0, fq[0]);
 #pragma unroll
-      for (int p = 0; p < 3; ++p) fa[p] = *reinterpret_cast<const bf16x8*>(sa + a * 32 * kRec + 16 * p);
+    for (int a = 0; a < Gm::kRB; ++a) {
+      if constexpr (BATCH == 1) {
+        if (a + 1 < Gm::kRB) read_block(a + 1, fq[(a + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+      } else if (a % BATCH == 0) {
+#pragma unroll
+        for (int u = 0; u < BATCH; ++u) read_block(a + u, fq[u]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      const bf16x8 (&fa)[3] = fq[BATCH == 1 ? (a & 1) : (a % BATCH)];
       f32x16 c = acc[a];  // the six piece products of one 32x32x16 block, smallest first (as dense_split3_kernel)
       c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2], fb[0], c, 0, 0, 0);
       c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[2], c, 0, 0, 0);
@@ -554,16 +599,21 @@ void dense_split3_fx8_kernel(const uint8_t* __restrict__ WA, float* __restrict__
       c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[1], c, 0, 0, 0);
       c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[0], c, 0, 0, 0);
       acc[a] = c;
+      if (a == (Gm::kRB > 1 ? 1 : 0) && s + 1 < n_stages) split_b(s + 1, vn, fn);  // under this step's MFMAs
     }
     __builtin_amdgcn_s_setprio(0);
+    if (s + 1 < n_stages) {
+#pragma unroll
+      for (int p = 0; p < 3; ++p) fb[p] = fn[p];
+    }
   }
   // C/D map (gfx950): col = lane & 31, row = (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5)
-  const int64_t col = col0 + mycol;
+  const int64_t col = col0 + li;
 #pragma unroll
-  for (int a = 0; a < 8; ++a)
+  for (int a = 0; a < Gm::kRB; ++a)
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
-      const int row = mt * kTile + a * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+      const int row = mt * kTile + wm * 32 * Gm::kRB + a * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
       if (row < M && col < P) __builtin_nontemporal_store(acc[a][e], Y + int64_t(row) * ldy + col);
     }
 }
@@ -702,8 +752,18 @@ extern "C" int dol_mix_dense_split3_f32(const float* W, int64_t ldw, const float
                          static_cast<int>(g.Kg / 2), n_mt, n_pt, tiles_per_xcd, group_m, X, ldx, K, pread, t_base,
                          t_end);
     };
-    launch8(dense_split3_fx8_kernel<8>, kStages * Fx8Geom<8>::kStage, grid, 0, t_main, 512);
-    if (fx8_tail) launch8(dense_split3_fx8_kernel<2>, kStages * Fx8Geom<2>::kStage, 4 * tail, t_main, n_tiles, 128);
+    // DOL_SPLIT3_FX8_BATCH (read per call; A fragment batching, same bits): 1 (default), 2 or 4
+    const char* be = getenv("DOL_SPLIT3_FX8_BATCH");
+    const int batch = be ? atoi(be) : 1;
+    if (batch == 4) launch8(dense_split3_fx8_kernel<1, 8, 4>, kStages * Fx8Geom<1, 8>::kStage, grid, 0, t_main, 512);
+    else if (batch == 2) launch8(dense_split3_fx8_kernel<1, 8, 2>, kStages * Fx8Geom<1, 8>::kStage, grid, 0, t_main, 512);
+    else launch8(dense_split3_fx8_kernel<1, 8>, kStages * Fx8Geom<1, 8>::kStage, grid, 0, t_main, 512);
+    // the tail's quarter tiles: DOL_SPLIT3_FX8_TAIL (read per call; same bits) 8 = 4 x 2 waves (default), 4 = 2 x 2
+    const char* te = getenv("DOL_SPLIT3_FX8_TAIL");
+    if (fx8_tail && te && atoi(te) == 4)
+      launch8(dense_split3_fx8_kernel<2, 2>, kStages * Fx8Geom<2, 2>::kStage, 4 * tail, t_main, n_tiles, 256);
+    else if (fx8_tail)
+      launch8(dense_split3_fx8_kernel<4, 2>, kStages * Fx8Geom<4, 2>::kStage, 4 * tail, t_main, n_tiles, 512);
     return dol::check_launch("dol_mix_dense_split3_f32");
   }
   if (fx) {

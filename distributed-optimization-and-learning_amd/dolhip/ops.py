@@ -576,11 +576,14 @@ def dense_split3_workspace_bytes(M: int, K: int, P: int, flags: int = 0) -> int:
 
 def mix_dense_split3(W: torch.Tensor, X: torch.Tensor, Y: torch.Tensor, P: Optional[int] = None,
                      work: Optional[torch.Tensor] = None, w_ready: bool = False,
-                     fuse: bool = False) -> torch.Tensor:
+                     fuse: Optional[bool] = None) -> torch.Tensor:
     """Y = W X on the bf16 matrix cores at fp32 accuracy (dol_mix_dense_split3_f32:
     three-piece bf16 split of both operands, six piece products per term).
-    fuse=True splits X inside the GEMM when its rows allow (no X workspace,
-    slower; same bits) instead of in a split pass.  `work`: a uint8 device
+    fuse (None = when X's rows allow it, split3_x_flags): X is split inside
+    the GEMM (dense_split3_fx8_kernel: no split pass, no X workspace; same
+    bits) instead of by a split pass -- at 1024 x 101,770 0.94-0.95 vs
+    1.04 ms a round (tools/split3_ab.py, profiles/r05m_split3_ab.jsonl).
+    fuse=False forces the split pass.  `work`: a uint8 device
     buffer of >= dense_split3_workspace_bytes(M, K, P, flags) bytes (allocated
     per call when None); w_ready=True reuses the split W that a previous call
     with the same W left in `work`."""
@@ -593,7 +596,9 @@ def mix_dense_split3(W: torch.Tensor, X: torch.Tensor, Y: torch.Tensor, P: Optio
         raise ValueError(f"shapes: W {tuple(W.shape)}, X {tuple(X.shape)}, Y {tuple(Y.shape)}")
     if Y.data_ptr() in (X.data_ptr(), W.data_ptr()):
         raise ValueError("Y aliases an input")
-    flags = ((SPLIT3_FUSE_X | split3_x_flags(X, P)) if fuse else 0) | (SPLIT3_W_READY if w_ready else 0)
+    xf = split3_x_flags(X, P) if fuse is not False else 0
+    fused = bool(xf) or (fuse is True and P % 4 == 0)
+    flags = ((SPLIT3_FUSE_X | xf) if fused else 0) | (SPLIT3_W_READY if w_ready else 0)
     need = dense_split3_workspace_bytes(M, K, P, flags)
     if work is None:
         if w_ready:

@@ -438,9 +438,10 @@ def test_mix_dense_split3_matches_f32_kernel_and_ragged_rows(gpu):
     assert e_split.max() <= 2 * e_f32.max() + 1e-30
 
 
+@pytest.mark.parametrize("fuse", [False, None])
 @pytest.mark.parametrize("M,K,P,cus", [(300, 300, 2148, 16), (256, 777, 5137, 20), (513, 64, 3001, 32),
                                        (300, 300, 2148, 14), (513, 64, 3001, 10), (1024, 1024, 101770, None)])
-def test_mix_dense_split3_narrow_tail_bit_identical(M, K, P, cus, gpu, monkeypatch):
+def test_mix_dense_split3_narrow_tail_bit_identical(M, K, P, cus, fuse, gpu, monkeypatch):
     """The last partial wave of 256 x 256 tiles runs as 256 x 64 quarters
     (dense_split3_kernel<.., NB = 1>) when it would fill <= 1/4 of the CUs, as
     256 x 128 halves (NB = 2) when <= 1/2 (cus = 14, 10 here);
@@ -457,9 +458,9 @@ def test_mix_dense_split3_narrow_tail_bit_identical(M, K, P, cus, gpu, monkeypat
         monkeypatch.delenv("DOL_SPLIT3_CUS", raising=False)
     else:
         monkeypatch.setenv("DOL_SPLIT3_CUS", str(cus))
-    ops.mix_dense_split3(Wd, Xd, Y1, P=P)
+    ops.mix_dense_split3(Wd, Xd, Y1, P=P, fuse=fuse)  # None: the default (fused where the rows allow)
     monkeypatch.setenv("DOL_SPLIT3_CUS", "0")
-    ops.mix_dense_split3(Wd, Xd, Y2, P=P)
+    ops.mix_dense_split3(Wd, Xd, Y2, P=P, fuse=fuse)
     torch.cuda.synchronize()
     assert bits_equal(Y1[:, :P].cpu().numpy(), Y2[:, :P].cpu().numpy())
     assert np.isnan(Y1[:, P:].cpu().numpy()).all()
@@ -486,7 +487,7 @@ def test_mix_dense_split3_fused_x_equals_split_pass(M, K, P, extra, gpu):
     assert fused == (((P + extra) % 4 == 0) and P >= 4)
     Y1, Y2 = padded(np.zeros((M, P), np.float32), gpu, extra), padded(np.zeros((M, P), np.float32), gpu, extra)
     ops.mix_dense_split3(Wd, Xd, Y1, P=P, fuse=True)
-    ops.mix_dense_split3(Wd, Xd, Y2, P=P)
+    ops.mix_dense_split3(Wd, Xd, Y2, P=P, fuse=False)
     torch.cuda.synchronize()
     a, b = Y1[:, :P].cpu().numpy(), Y2[:, :P].cpu().numpy()
     assert bits_equal(a, b)
@@ -519,10 +520,14 @@ def test_mix_dense_split3_fx8_tiles_and_tail_bit_identical(M, K, P, cus, gpu, mo
     else:
         monkeypatch.setenv("DOL_SPLIT3_CUS", str(cus))
     ops.mix_dense_split3(Wd, Xd, Y1, P=P, fuse=True)
-    ops.mix_dense_split3(Wd, Xd, Y2, P=P)
+    ops.mix_dense_split3(Wd, Xd, Y2, P=P, fuse=False)
     torch.cuda.synchronize()
     assert bits_equal(Y1[:, :P].cpu().numpy(), Y2[:, :P].cpu().numpy())
     assert np.isnan(Y1[:, P:].cpu().numpy()).all()
+    Y3 = padded(np.zeros((M, P), np.float32), gpu, 3)
+    ops.mix_dense_split3(Wd, Xd, Y3, P=P)  # the default picks the fused path for these rows: same bits
+    torch.cuda.synchronize()
+    assert bits_equal(Y3[:, :P].cpu().numpy(), Y2[:, :P].cpu().numpy())
 
 
 def _er_hip_numpy(n, p, seed):

@@ -28,7 +28,10 @@ def main():
         ops.mix_dense_split3(W, X, Y, P=P, work=work)
     torch.cuda.synchronize()
     for rep in range(4):
-        for fuse in (False, True):
+        for fuse, batch, tail in ((False, None, None), (True, "1", "8"), (True, "4", "8"), (True, "4", "4")):
+            if batch is not None:  # read per call by dol_mix_dense_split3_f32
+                os.environ["DOL_SPLIT3_FX8_BATCH"] = batch
+                os.environ["DOL_SPLIT3_FX8_TAIL"] = tail
             for _ in range(20):
                 ops.mix_dense_split3(W, X, Y, P=P, work=work, fuse=fuse)
             torch.cuda.synchronize()
@@ -39,7 +42,7 @@ def main():
             e.record()
             torch.cuda.synchronize()
             ms = s.elapsed_time(e) / 20
-            print(json.dumps({"rep": rep, "agents": N, "params": P, "fused_x": fuse, "ms": ms,
+            print(json.dumps({"rep": rep, "agents": N, "params": P, "fused_x": fuse, "fx8_batch": batch, "fx8_tail_waves": tail, "ms": ms,
                               "bf16_mfma_util": 6 * 2.0 * N * N * P / (ms / 1e3) / 1e12 / 2516.6}), flush=True)
 
 
