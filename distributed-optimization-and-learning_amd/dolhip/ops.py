@@ -574,16 +574,22 @@ def dense_split3_workspace_bytes(M: int, K: int, P: int, flags: int = 0) -> int:
     return int(_native.lib().dol_mix_dense_split3_workspace_bytes(int(M), int(K), int(P), int(flags)))
 
 
+SPLIT3_FUSE_MAX_M = 2048  # auto-fused X split up to this many output rows (agents)
+
+
 def mix_dense_split3(W: torch.Tensor, X: torch.Tensor, Y: torch.Tensor, P: Optional[int] = None,
                      work: Optional[torch.Tensor] = None, w_ready: bool = False,
                      fuse: Optional[bool] = None) -> torch.Tensor:
     """Y = W X on the bf16 matrix cores at fp32 accuracy (dol_mix_dense_split3_f32:
     three-piece bf16 split of both operands, six piece products per term).
-    fuse (None = when X's rows allow it, split3_x_flags): X is split inside
-    the GEMM (dense_split3_fx8_kernel: no split pass, no X workspace; same
-    bits) instead of by a split pass -- at 1024 x 101,770 0.94-0.95 vs
-    1.04 ms a round (tools/split3_ab.py, profiles/r05m_split3_ab.jsonl).
-    fuse=False forces the split pass.  `work`: a uint8 device
+    fuse (None = when X's rows allow it, split3_x_flags, and M <=
+    SPLIT3_FUSE_MAX_M): X is split inside the GEMM (dense_split3_fx8_kernel:
+    no split pass, no X workspace; same bits) instead of by a split pass.  Its
+    GEMM runs ~6-8 % slower than the record-staged one, so it pays where the
+    pass is a large share of the round, i.e. few output rows per X value:
+    1024 x 1024 x 101,770 0.94-0.95 vs 1.04 ms, 8192 x 8192 x 101,770 56.2
+    vs 53.1 ms (tools/split3_ab.py, profiles/r05m_split3_ab.jsonl,
+    r05n_split3_ab_8192.jsonl).  fuse=False forces the split pass.  `work`: a uint8 device
     buffer of >= dense_split3_workspace_bytes(M, K, P, flags) bytes (allocated
     per call when None); w_ready=True reuses the split W that a previous call
     with the same W left in `work`."""
@@ -596,6 +602,8 @@ def mix_dense_split3(W: torch.Tensor, X: torch.Tensor, Y: torch.Tensor, P: Optio
         raise ValueError(f"shapes: W {tuple(W.shape)}, X {tuple(X.shape)}, Y {tuple(Y.shape)}")
     if Y.data_ptr() in (X.data_ptr(), W.data_ptr()):
         raise ValueError("Y aliases an input")
+    if fuse is None:
+        fuse = None if W.shape[0] <= SPLIT3_FUSE_MAX_M else False
     xf = split3_x_flags(X, P) if fuse is not False else 0
     fused = bool(xf) or (fuse is True and P % 4 == 0)
     flags = ((SPLIT3_FUSE_X | xf) if fused else 0) | (SPLIT3_W_READY if w_ready else 0)
