@@ -646,6 +646,173 @@ inline bool fused_x_ok(const float* X, int64_t ldx, int64_t P, int flags) {
   return (flags & DOL_SPLIT3_FUSE_X) && aligned && P >= 4 && (P % 4 == 0 || (flags & DOL_SPLIT3_X_ROWS_PADDED));
 }
 
+
+// FXW (r05): the split-pass kernel's 2 x 4 waves and fragment reads (12 A + 6
+// B ds_read_b128 per wave and k-step, the fewest of any layout), with the B
+// records made in the kernel instead of by the split pass.  Each of the 512
+// lanes owns one (8 k x 1 column) record of a k-step; each wave stages the X
+// rows of its own 64 records by LDS-DMA (8 rows x 256 B, two 1-KiB pieces,
+// two stages), so after its own vmcnt wait -- no barrier -- it reads its 8
+// values (ds_read_b32, conflict-free), splits them under the current step's
+// MFMAs (split8: the split pass's bits) and writes the 48-B record into the
+// other half of a double-buffered B stage, which every wave reads after the
+// next step's barrier.  LDS: 3 x 24 KiB of A + 2 x 16 KiB of X + 2 x 24 KiB
+// of B records = 152 KiB.  Same k-steps, same fragments, same six MFMAs per
+// block in the same order as dense_split3_kernel: bit-identical.
+constexpr int kFxwX = 16 * 1024;                                         // one X stage: 8 waves x 8 rows x 256 B
+constexpr int kFxwLds = kStages * kOpStage + 2 * kFxwX + 2 * kOpStage;    // 152 KiB
+static_assert(kFxwLds <= 160 * 1024, "LDS budget");
+
+constexpr int kFxwSplitAt = 1;  // the split after row block 1's MFMAs (0 / 2 / 3 measured 1-2 % slower)
+
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void dense_split3_fxw_kernel(const uint8_t* __restrict__ WA, float* __restrict__ Y, int64_t ldy, int M, int64_t P,
+                             int64_t Mp, int n_stages, int n_mt, int64_t n_pt, int64_t tiles_per_xcd, int group_m,
+                             const float* __restrict__ X, int64_t ldx, int K, int64_t pread, int64_t t_base,
+                             int64_t t_end) {
+  (void)t_base;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int64_t jt = blockIdx.x >> 3;
+  const int64_t t = (blockIdx.x & 7) * tiles_per_xcd + jt;
+  if (jt >= tiles_per_xcd || t >= t_end) return;
+  const int64_t per_group = int64_t(group_m) * n_pt;
+  const int g = int(t / per_group);
+  const int first_m = g * group_m;
+  const int gs = min(n_mt - first_m, group_m);
+  const int64_t r = t - int64_t(g) * per_group;
+  const int mt = first_m + int(r % gs);
+  const int64_t pt = r / gs;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int h = lane >> 5, li = lane & 31;
+  const uint8_t* srcA = WA + int64_t(mt) * kTile * kRec + lane * 16;
+  const int64_t pitchA = Mp * kRec;
+  const int64_t col0 = pt * kTile;
+  // X DMA: each wave stages the rows of its own records (k-group rkg, 64 columns), so the
+  // split needs only the wave's own vmcnt, no barrier; lane: row lane / 16, 16 B at column 4 (lane % 16)
+  int64_t cdma = col0 + ((wave & 3) << 6) + 4 * (lane & 15);  // past P: clamped, masked after the read
+  if (cdma + 4 > pread) cdma = pread - 4;
+  uint8_t* const ringA = lds;
+  uint8_t* const ringX = lds + kStages * kOpStage;
+  uint8_t* const ringB = ringX + 2 * kFxwX;
+  // this lane's record of every k-step: k-group rkg of the step, tile column rp
+  const int rkg = wave >> 2, rp = ((wave & 3) << 6) + lane;
+  const bool cok = col0 + rp < P;
+  uint8_t* const rec = ringB + rkg * (kTile * kRec) + rp * kRec;
+
+  // step group s, in issue order: X(s) 2 DMAs, A(s) 3 DMAs per wave
+  auto issue = [&](int s) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {  // rows 8 rkg + 4 i .. + 3 of this wave's 64 columns: 4 x 256 B
+      const int k = min(16 * s + 8 * rkg + 4 * i + (lane >> 4), K - 1);  // rows past K: clamped, masked after the read
+      __builtin_amdgcn_global_load_lds(DOL_GPTR(X + int64_t(k) * ldx + cdma),
+                                       DOL_LPTR(ringX + (s & 1) * kFxwX + wave * 2048 + i * 1024), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int q = wave + 8 * i;
+      const uint8_t* src = srcA + (2 * int64_t(s) + q / 12) * pitchA + (q % 12) * 1024;
+      __builtin_amdgcn_global_load_lds(DOL_GPTR(src), DOL_LPTR(ringA + (s % kStages) * kOpStage + q * 1024), 16, 0, 0);
+    }
+  };
+  auto read_x = [&](int s, float (&v)[8]) {  // step s's record of this lane from X stage s % 2 (row j at j * 256 B)
+    const float* xs = reinterpret_cast<const float*>(ringX + (s & 1) * kFxwX + wave * 2048) + lane;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = xs[j * 64];
+  };
+  auto split_x = [&](int s, float (&v)[8]) {  // ... split into B stage s % 2
+    if (!cok || 16 * s + 16 > K) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (cok && 16 * s + 8 * rkg + j < K) ? v[j] : 0.f;
+    }
+    bf16x8 q0, q1, q2;
+    split8(v, q0, q1, q2);
+    uint8_t* d = rec + (s & 1) * kOpStage;
+    *reinterpret_cast<bf16x8*>(d) = q0;
+    *reinterpret_cast<bf16x8*>(d + 16) = q1;
+    *reinterpret_cast<bf16x8*>(d + 32) = q2;
+  };
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.f;
+
+  issue(0);
+  if (n_stages > 1) {
+    issue(1);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // my X(0) rows landed (A(0) and group 1 may fly)
+  } else {
+    asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  }
+  {
+    float v0[8];
+    read_x(0, v0);
+    split_x(0, v0);
+  }
+  for (int s = 0; s < n_stages; ++s) {
+    // A(s) landed: after it only group s + 1 may fly.  lgkmcnt(0): this wave's
+    // record writes and fragment reads are done before the barrier
+    if (s + 1 < n_stages) asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's A(s) and B records of s are in LDS
+    asm volatile("" ::: "memory");
+    if (s + 2 < n_stages) issue(s + 2);  // X slot s % 2 (my rows, split during s - 1), A slot (s + 2) % 3: free
+    const uint8_t* sa = ringA + (s % kStages) * kOpStage + h * (kTile * kRec) + (wm * 128 + li) * kRec;
+    const uint8_t* sb = ringB + (s & 1) * kOpStage + h * (kTile * kRec) + (wn * 64 + li) * kRec;
+    bf16x8 fa[4][3], fb[2][3];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) fa[i][p] = *reinterpret_cast<const bf16x8*>(sa + i * 32 * kRec + 16 * p);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) fb[i][p] = *reinterpret_cast<const bf16x8*>(sb + i * 32 * kRec + 16 * p);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        f32x16 c = acc[a][b];  // six piece products, smallest first (as dense_split3_kernel)
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a][2], fb[b][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a][0], fb[b][2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a][1], fb[b][1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a][1], fb[b][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a][0], fb[b][1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a][0], fb[b][0], c, 0, 0, 0);
+        acc[a][b] = c;
+      }
+      if (a == kFxwSplitAt && s + 1 < n_stages) {  // step s + 1's record, under this step's MFMAs
+        // my X(s + 1) rows landed: after them A(s + 1) and group s + 2 may fly
+        if (s + 2 < n_stages) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        float xv[8];
+        read_x(s + 1, xv);
+        split_x(s + 1, xv);
+      }
+    }
+    __builtin_amdgcn_s_setprio(0);
+  }
+  // C/D map (gfx950): col = lane & 31, row = (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5)
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int64_t col = col0 + wn * 64 + b * 32 + li;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = mt * kTile + wm * 128 + a * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (row < M && col < P) __builtin_nontemporal_store(acc[a][b][e], Y + int64_t(row) * ldy + col);
+      }
+    }
+}
+
 }  // namespace
 
 extern "C" int64_t dol_mix_dense_split3_workspace_bytes(int32_t M, int32_t K, int64_t P, int flags) {
@@ -755,7 +922,11 @@ extern "C" int dol_mix_dense_split3_f32(const float* W, int64_t ldw, const float
     // DOL_SPLIT3_FX8_BATCH (read per call; A fragment batching, same bits): 1 (default), 2 or 4
     const char* be = getenv("DOL_SPLIT3_FX8_BATCH");
     const int batch = be ? atoi(be) : 1;
-    if (batch == 4) launch8(dense_split3_fx8_kernel<1, 8, 4>, kStages * Fx8Geom<1, 8>::kStage, grid, 0, t_main, 512);
+    // main tiles: dense_split3_fxw_kernel (r05; 864-872 vs 884-887 us for FX8's 1 x 8 layout at
+    // 1024 x 101,770, profiles/r05x_split3_fxw_ab.jsonl) unless DOL_SPLIT3_FXW=0 (read per call; same bits)
+    const char* we = getenv("DOL_SPLIT3_FXW");
+    if (!(we && atoi(we) == 0)) launch8(dense_split3_fxw_kernel, kFxwLds, grid, 0, t_main, 512);
+    else if (batch == 4) launch8(dense_split3_fx8_kernel<1, 8, 4>, kStages * Fx8Geom<1, 8>::kStage, grid, 0, t_main, 512);
     else if (batch == 2) launch8(dense_split3_fx8_kernel<1, 8, 2>, kStages * Fx8Geom<1, 8>::kStage, grid, 0, t_main, 512);
     else launch8(dense_split3_fx8_kernel<1, 8>, kStages * Fx8Geom<1, 8>::kStage, grid, 0, t_main, 512);
     // the tail's quarter tiles: DOL_SPLIT3_FX8_TAIL (read per call; same bits) 8 = 4 x 2 waves (default), 4 = 2 x 2

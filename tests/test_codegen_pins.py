@@ -27,11 +27,10 @@ CSRC = os.path.join(ROOT, "distributed-optimization-and-learning_amd", "csrc")
 LLVM = "/opt/rocm/lib/llvm/bin"
 
 
-@pytest.fixture(scope="module")
-def code_object(tmp_path_factory):
-    obj = os.path.join(CSRC, "obj", "dol_hip.o")
+def _unbundle(name, tmp_path_factory):
+    obj = os.path.join(CSRC, "obj", name)
     if not os.path.exists(obj):
-        subprocess.run(["make", "-s", "-C", CSRC, "obj/dol_hip.o"], check=True)
+        subprocess.run(["make", "-s", "-C", CSRC, f"obj/{name}"], check=True)
     bundler = os.path.join(LLVM, "clang-offload-bundler")
     if not os.path.exists(bundler):
         pytest.skip("clang-offload-bundler not found")
@@ -41,6 +40,16 @@ def code_object(tmp_path_factory):
     subprocess.run([bundler, "--type=o", "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--input={fat}",
                     f"--output={co}", "--unbundle"], check=True)
     return co
+
+
+@pytest.fixture(scope="module")
+def code_object(tmp_path_factory):
+    return _unbundle("dol_hip.o", tmp_path_factory)
+
+
+@pytest.fixture(scope="module")
+def split_code_object(tmp_path_factory):
+    return _unbundle("dense_split.o", tmp_path_factory)
 
 
 def _kernels(co, stem):
@@ -82,3 +91,20 @@ def test_device_build_refuses_other_targets():
     r = subprocess.run([hipcc, "--offload-arch=gfx942", "--cuda-device-only", "-c", "-x", "hip", "-", "-I", CSRC,
                         "-o", os.devnull], input=src, capture_output=True, text=True)
     assert r.returncode != 0 and "written for gfx950" in (r.stderr + r.stdout)
+
+
+def test_split3_fxw_waits_are_counted(split_code_object):
+    """dense_split3_fxw_kernel (r05) counts its LDS-DMA groups (X 2 + A 3 per
+    wave and k-step) with fixed waits: vmcnt(5) before the barrier (A(s) in,
+    group s + 1 in flight), vmcnt(8) / vmcnt(3) before the in-loop split (this
+    wave's X(s + 1) rows in), vmcnt(0) at the last step; any other wait, a
+    separate store counter or extra vector-memory ops in the k-loop would
+    break the accounting or the overlap."""
+    ks = _kernels(split_code_object, "dense_split3_fxw_kernel")
+    assert len(ks) == 1, ks
+    asm = _disasm(split_code_object, ks[0])
+    waits = set(int(v) for v in re.findall(r"s_waitcnt vmcnt\((\d+)\)", asm))
+    assert {5, 8} <= waits <= {0, 3, 5, 8}, sorted(waits)
+    assert "vscnt" not in asm
+    assert len(re.findall(r"global_load_lds_dwordx4", asm)) >= 10  # prologue groups 0 and 1 (+ the loop's)
+    assert not re.search(r"global_load_dword[^x_]|global_load_dwordx[24]\b|buffer_load", asm), "unexpected vector loads"

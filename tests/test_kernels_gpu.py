@@ -469,13 +469,17 @@ def test_mix_dense_split3_narrow_tail_bit_identical(M, K, P, cus, fuse, gpu, mon
         assert np.all(np.abs(Y1[:, :P].cpu().numpy() - want64) <= _split3_bound(W, X) + 1e-30)
 
 
+@pytest.mark.parametrize("main", ["fxw", "fx8"])
 @pytest.mark.parametrize("M,K,P,extra", [(256, 256, 1024, 0), (130, 37, 1031, 1), (300, 600, 5000, 4),
                                          (64, 20, 4, 0), (513, 300, 701, 3), (200, 50, 999, 0)])
-def test_mix_dense_split3_fused_x_equals_split_pass(M, K, P, extra, gpu):
-    """X split in registers inside the GEMM (rows 16-B readable) gives the same
-    bits as the split pass, at ragged K / P tiles, NaN padding past P, values
-    near the bf16 overflow threshold (the wave's scalar fallback), subnormals
-    and signed zeros; ld % 4 != 0 falls back to the split pass."""
+def test_mix_dense_split3_fused_x_equals_split_pass(M, K, P, extra, main, gpu, monkeypatch):
+    """X split inside the GEMM (rows 16-B readable) gives the same bits as the
+    split pass, at ragged K / P tiles, NaN padding past P, values near the bf16
+    overflow threshold (the wave's scalar fallback), subnormals and signed
+    zeros; ld % 4 != 0 falls back to the split pass.  Main tiles on
+    dense_split3_fxw_kernel (default) or dense_split3_fx8_kernel
+    (DOL_SPLIT3_FXW=0, read per call)."""
+    monkeypatch.setenv("DOL_SPLIT3_FXW", "0" if main == "fx8" else "1")
     rng = np.random.default_rng(M * 7 + K)
     W = ((rng.random((M, K)) < 0.3) * rng.random((M, K))).astype(np.float32)
     X = rng.standard_normal((K, P)).astype(np.float32)
@@ -499,15 +503,19 @@ def test_mix_dense_split3_fused_x_equals_split_pass(M, K, P, extra, gpu):
     assert np.all(err <= _split3_bound(W[ok], X) + 1e-30)
 
 
+@pytest.mark.parametrize("main", ["fxw", "fx8"])
 @pytest.mark.parametrize("M,K,P,cus", [(300, 300, 2148, 16), (513, 64, 3001, 32), (256, 777, 5137, 0),
                                        (1024, 1024, 101770, None)])
-def test_mix_dense_split3_fx8_tiles_and_tail_bit_identical(M, K, P, cus, gpu, monkeypatch):
-    """dense_split3_fx8_kernel (r05, the fused X split: each wave splits its own
-    32 columns once and runs 8 row blocks) on 256 x 256 tiles and, for the last
-    partial wave of tiles, 256 x 64 quarters (DOL_SPLIT3_CUS pretends a CU
-    count so small shapes take that path; None: the device's own, 1592 tiles at
-    the bench's 1024 x 101,770): the same bits as the split pass + the
+def test_mix_dense_split3_fx8_tiles_and_tail_bit_identical(M, K, P, cus, main, gpu, monkeypatch):
+    """The fused X split (r05) on 256 x 256 tiles -- dense_split3_fxw_kernel
+    (default: the record kernel's 2 x 4 waves, each lane splitting one record
+    into LDS) or dense_split3_fx8_kernel (DOL_SPLIT3_FXW=0: each wave splits
+    its own 32 columns once and runs 8 row blocks) -- and, for the last partial
+    wave of tiles, FX8's 256 x 64 quarters (DOL_SPLIT3_CUS pretends a CU count
+    so small shapes take that path; None: the device's own, 1592 tiles at the
+    bench's 1024 x 101,770): the same bits as the split pass + the
     record-staged GEMM, padding past P untouched."""
+    monkeypatch.setenv("DOL_SPLIT3_FXW", "0" if main == "fx8" else "1")
     rng = np.random.default_rng(M + 3 * K + P)
     W = ((rng.random((M, K)) < 0.2) * rng.random((M, K))).astype(np.float32)
     X = rng.standard_normal((K, P)).astype(np.float32)

@@ -1,5 +1,6 @@
 """Dense ER mix on the bf16 matrix cores (split3): the split pass + record-staged
-GEMM vs the fused X split (dense_split3_fx8_kernel, r05), alternating in one
+GEMM vs the fused X split (dense_split3_fx8_kernel and dense_split3_fxw_kernel,
+r05; DOL_SPLIT3_FXW=1 selects the latter), alternating in one
 process at bench.dense_mix_round's shape (1024 agents x 101,770, ER p = 0.1,
 ld = row_stride(P)); one JSON line per (rep, path) with ms and the bf16 MFMA
 utilisation the bench reports (6 x 2 N^2 P flop / ms / 2516.6 TF)."""
@@ -28,10 +29,9 @@ def main():
         ops.mix_dense_split3(W, X, Y, P=P, work=work)
     torch.cuda.synchronize()
     for rep in range(4):
-        for fuse, batch, tail in ((False, None, None), (True, "1", "8"), (True, "4", "8"), (True, "4", "4")):
-            if batch is not None:  # read per call by dol_mix_dense_split3_f32
-                os.environ["DOL_SPLIT3_FX8_BATCH"] = batch
-                os.environ["DOL_SPLIT3_FX8_TAIL"] = tail
+        for path, fuse, env in (("split_pass", False, {}), ("fx8", True, {"DOL_SPLIT3_FXW": "0"}),
+                                ("fxw", True, {"DOL_SPLIT3_FXW": "1"})):
+            os.environ.update(env)  # read per call by dol_mix_dense_split3_f32
             for _ in range(20):
                 ops.mix_dense_split3(W, X, Y, P=P, work=work, fuse=fuse)
             torch.cuda.synchronize()
@@ -42,7 +42,7 @@ def main():
             e.record()
             torch.cuda.synchronize()
             ms = s.elapsed_time(e) / 20
-            print(json.dumps({"rep": rep, "agents": N, "params": P, "fused_x": fuse, "fx8_batch": batch, "fx8_tail_waves": tail, "ms": ms,
+            print(json.dumps({"rep": rep, "agents": N, "params": P, "path": path, "ms": ms,
                               "bf16_mfma_util": 6 * 2.0 * N * N * P / (ms / 1e3) / 1e12 / 2516.6}), flush=True)
 
 
