@@ -663,7 +663,9 @@ constexpr int kFxwX = 16 * 1024;                                         // one 
 constexpr int kFxwLds = kStages * kOpStage + 2 * kFxwX + 2 * kOpStage;    // 152 KiB
 static_assert(kFxwLds <= 160 * 1024, "LDS budget");
 
-constexpr int kFxwSplitAt = 1;  // the split after row block 1's MFMAs (0 / 2 / 3 measured 1-2 % slower)
+// the split after row block 1's MFMAs: after 0 / 2 / 3 measured 1-2 % slower, before the
+// MFMAs (in the barrier bubble, X reads ahead of the fragment reads) 4 % slower
+constexpr int kFxwSplitAt = 1;
 
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2)))
 void dense_split3_fxw_kernel(const uint8_t* __restrict__ WA, float* __restrict__ Y, int64_t ldy, int M, int64_t P,
