@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--agents", type=int, default=8192)
     ap.add_argument("--params", type=int, default=1 << 20)
     ap.add_argument("--ld", type=int, default=0, help="row stride in floats (0: ShardedRing's row_stride(P))")
+    ap.add_argument("--directions", action="store_true",
+                    help="each variant X -> Y ('v>'), Y -> X ('v<') and alternating as FedLCon's bank.mix swaps ('v~')")
     a = ap.parse_args()
     dev = torch.device("cuda")
     N, P = a.agents, a.params
@@ -46,13 +48,23 @@ def main():
         torch.cuda.synchronize()
         return s.elapsed_time(e) / a.reps
 
-    res = {str(v): [] for v in a.variants}
-    res["ring"] = []
+    res = {"ring": []}
     for _ in range(a.blocks):
         res["ring"].append(timed(lambda: ops.mix_ring(X, Y, ring.w_prev, ring.w_next, P=P, n_rows=N)))
         for v in a.variants:
-            res[str(v)].append(timed(lambda: ops.mix_ring_steps(X, Y, ring.w_prev, ring.w_next, a.eps, P=P, n_rows=N,
-                                                                variant=v)))
+            def run(src, dst):
+                return lambda: ops.mix_ring_steps(src, dst, ring.w_prev, ring.w_next, a.eps, P=P, n_rows=N, variant=v)
+            if not a.directions:
+                res.setdefault(str(v), []).append(timed(run(X, Y)))
+                continue
+            res.setdefault(f"{v}>", []).append(timed(run(X, Y)))
+            res.setdefault(f"{v}<", []).append(timed(run(Y, X)))
+            flip = [X, Y]
+
+            def alt():
+                ops.mix_ring_steps(flip[0], flip[1], ring.w_prev, ring.w_next, a.eps, P=P, n_rows=N, variant=v)
+                flip.reverse()
+            res.setdefault(f"{v}~", []).append(timed(alt))
     best = {k: min(v) for k, v in res.items()}
     print(json.dumps({"eps": a.eps, "agents": N, "params": P, "ld": X.stride(0),
                       "dma_d": os.environ.get("DOL_RING_DMA_D", "8"),
