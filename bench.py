@@ -378,17 +378,30 @@ def fedlcon_eps_round(device, ring, N: int, P: int, eps: int = 5, reps: int = 10
     torch.cuda.synchronize(device)
     ms_pass = _events_ms(lambda: bank.mix(plan, steps=eps), reps)
     entry = ops.ring_steps_choice(bank.x, bank.buffer("y"), eps, P=P, n_rows=N)
-    # the untuned library default on the same buffers, for comparison
-    ms_default = _events_ms(lambda: ops.mix_ring_steps(bank.x, bank.buffer("y"), plan.w_prev, plan.w_next, eps, P=P,
-                                                       n_rows=N, variant=0), reps)
-    ring.x, ring.y = bank.x, bank.buffer("y")  # (the buffers swapped an even or odd number of times)
     choice = entry["choice"] if entry else 0
+    bufs = [bank.x, bank.buffer("y")]
+
+    def alternating(variant):  # as bank.mix: each pass writes the other buffer
+        def run():
+            ops.mix_ring_steps(bufs[0], bufs[1], plan.w_prev, plan.w_next, eps, P=P, n_rows=N, variant=variant)
+            bufs.reverse()
+        return run
+    # the untuned library default on the same buffers, alternating like the product call
+    ms_default = _events_ms(alternating(0), reps)
+    # the pass per direction (one destination matrix of a pair can be the slow one)
+    a, b = bufs
+    direction_ms = {"x_to_y": _events_ms(lambda: ops.mix_ring_steps(a, b, plan.w_prev, plan.w_next, eps, P=P, n_rows=N,
+                                                                    variant=choice), reps),
+                    "y_to_x": _events_ms(lambda: ops.mix_ring_steps(b, a, plan.w_prev, plan.w_next, eps, P=P, n_rows=N,
+                                                                    variant=choice), reps)}
+    ring.x, ring.y = bank.x, bank.buffer("y")  # (the buffers swapped an even or odd number of times)
     return {"eps": eps, "rounds_per_s": eps * 1e3 / ms_pass, "ms_per_pass": ms_pass,
             "GBps_per_pass": 2 * N * P * 4 / (ms_pass / 1e3) / 1e9,
             "frac_per_pass": 2 * N * P * 4 / (ms_pass / 1e3) / 1e9 / HBM_PEAK_GBPS,
             "kernel": RING_STEPS_KERNELS.get(choice, "library default"),
             "variant_ms": {str(k): v for k, v in (entry["ms"] if entry else {}).items()},
-            "default_ms_per_pass": ms_default, "call": "AgentBank.mix(plan, steps=5) (FedLCon.run's call)",
+            "default_ms_per_pass": ms_default, "direction_ms": direction_ms,
+            "call": "AgentBank.mix(plan, steps=5) (FedLCon.run's call)",
             "what": "FedLCon eps=5 consensus rounds fused into one HBM pass, bit-identical; the kernel tuned by the "
                     "product path for the bank's buffers on first use"}
 
