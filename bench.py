@@ -389,7 +389,7 @@ def fedlcon_eps_round(device, ring, N: int, P: int, eps: int = 5, reps: int = 10
     # the untuned library default on the same buffers, alternating like the product call
     ms_default = _events_ms(alternating(0), reps)
     # the pass per direction (one destination matrix of a pair can be the slow one)
-    a, b = bufs
+    a, b = bank.x, bank.buffer("y")
     direction_ms = {"x_to_y": _events_ms(lambda: ops.mix_ring_steps(a, b, plan.w_prev, plan.w_next, eps, P=P, n_rows=N,
                                                                     variant=choice), reps),
                     "y_to_x": _events_ms(lambda: ops.mix_ring_steps(b, a, plan.w_prev, plan.w_next, eps, P=P, n_rows=N,
