@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--variants", type=int, nargs="+", default=[3])
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--torch", action="store_true", help="torch-allocated matrices instead of mapped blocks")
+    ap.add_argument("--pm", action="store_true", help="also the parameter-major random 4-regular mix (config 3) per pair")
     ap.add_argument("--va-align", type=int, nargs="+", default=[0],
                     help="DOL_BANK_VA_ALIGN per block of three matrices (0: the granularity)")
     a = ap.parse_args()
@@ -50,7 +51,11 @@ def main():
         mats = {k: device_matrix(N, ld, dev, mapped=not a.torch) for k in "ABC"}
         for m in mats.values():
             m.normal_()
-        eps, ring = {}, {}
+        eps, ring, pm = {}, {}, {}
+        if a.pm:
+            from dolhip import graph as G
+            c = G.random_regular_csr(N, 4, seed=2028)
+            rr = [torch.as_tensor(t, device=dev) for t in (c.rowptr, c.col, c.val)]
         for src in "ABC":
             for dst in "ABC":
                 if src == dst:
@@ -60,8 +65,12 @@ def main():
                 eps[pair] = {v: timed(lambda: ops.mix_ring_steps(X, Y, wp, wn, 5, P=P, n_rows=N, variant=v))
                              for v in a.variants}
                 ring[pair] = timed(lambda: ops.mix_ring(X, Y, wp, wn, P=P, n_rows=N))
+                if a.pm:
+                    XT, YT = X.view(-1)[:P * N].view(P, N), Y.view(-1)[:P * N].view(P, N)
+                    pm.setdefault(pair, timed(lambda: ops.mix_csr_pm(XT, YT, *rr, nseg=16)))
                 print(json.dumps({"va_align": align, "pair": pair, "eps_ms": {v: round(t, 3) for v, t in eps[pair].items()},
-                                  "ring_ms": round(ring[pair], 3)}), file=sys.stderr, flush=True)
+                                  "ring_ms": round(ring[pair], 3), "pm_ms": round(pm.get(pair, 0.0), 3)}),
+                      file=sys.stderr, flush=True)
         print(json.dumps({"variants": a.variants, "band_r": os.environ.get("DOL_RING_BAND_R"),
                           "alloc": "torch" if a.torch else "mapped", "ld": ld, "va_align": align,
                           "bases": {k: m.data_ptr() for k, m in mats.items()}, "eps_ms": eps, "ring_ms": ring}),
