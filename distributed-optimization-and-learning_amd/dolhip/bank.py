@@ -160,9 +160,40 @@ def device_matrix(rows: int, cols: int, device, zero: bool = False, mapped: Opti
     return alloc(rows, cols, dtype=torch.float32, device=device)
 
 
+# Destination check of fused ring passes (r05): on some pairs of
+# large allocations the eps pass's column-strip read + write stream runs ~20 %
+# slower than on others (13.1-13.5 vs 11.0-11.4 ms at 8192 x 2^20, while the
+# ring round is 10.6-10.9 ms on every pair; which pairs is random per
+# allocation, any allocator).  Before a bank's fused pass first writes a
+# buffer from a given source, the pass and one ring round are timed on that
+# (source, destination) pair; when the pass is slower than PAIR_RATIO x the
+# round, the destination -- whose contents the pass is about to overwrite --
+# is replaced by a fresh allocation (up to PAIR_TRIES times, keeping the
+# fastest).  DOL_BANK_PAIR_PROBE=0 turns it off.
+PAIR_PROBE_MIN_BYTES = 4 << 30
+PAIR_RATIO = 1.12
+PAIR_TRIES = 3
+
+
+def _pair_probe_ms(x: torch.Tensor, y: torch.Tensor, plan, steps: int, P: int, reps: int = 2) -> Tuple[float, float]:
+    """(ms of the fused `steps`-round pass x -> y, ms of one ring round x -> y) on
+    the current stream; y is overwritten, x is only read."""
+    def one_pass():
+        ops.mix_ring_steps(x, y, plan.w_prev, plan.w_next, steps, P=P, n_rows=plan.n_rows, variant=3)
+
+    def one_round():
+        ops.mix_ring(x, y, plan.w_prev, plan.w_next, P=P, n_rows=plan.n_rows)
+    t = ops._time_each(lambda f: f(), [one_pass, one_round], reps, device=x.device)
+    return t[one_pass], t[one_round]
+
+
 class AgentBank:
     def __init__(self, n_agents: int, layout_or_P, device, ld: Optional[int] = None):
         self.device = torch.device(device)
+        # (source ptr, destination ptr) pairs whose fused-pass rate was checked; the probe log
+        self._pair_checked: set = set()
+        self.pair_probes: List[dict] = []
+        self._pair_timer = _pair_probe_ms  # tests inject a timer
         if isinstance(layout_or_P, int):
             self.layout: Layout = [("w", (int(layout_or_P),))]
         else:
@@ -272,6 +303,8 @@ class AgentBank:
         done = 0
         while done < steps:
             if fuse:
+                if steps - done > 1:
+                    y = self._check_destination(plan, min(steps - done, plan.MAX_FUSED_STEPS))
                 done += plan.apply_steps(self.buffer("x"), y, steps - done, P=self.P)
             else:
                 plan.apply(self.buffer("x"), y, P=self.P)
@@ -279,6 +312,36 @@ class AgentBank:
             self._buf["x"], self._buf["y"] = y, self._buf["x"]
             y = self._buf["y"]
         self.rebind_all()
+
+    def _check_destination(self, plan, steps: int) -> torch.Tensor:
+        """The buffer the next fused ring pass writes ("y"), replaced first if
+        its pair with "x" is one of the slow ones (see PAIR_RATIO above).  Only
+        for ring plans on large CUDA banks, once per (x, y) pair; y's contents
+        are dead (the pass overwrites them) and x is only read."""
+        y = self.buffer("y")
+        x = self.buffer("x")
+        if (getattr(plan, "kind", None) != "ring" or self.device.type != "cuda" or self.P % 4
+                or self.n * self.ld * 4 < PAIR_PROBE_MIN_BYTES or os.environ.get("DOL_BANK_PAIR_PROBE", "1") == "0"):
+            return y
+        if (x.data_ptr(), y.data_ptr()) in self._pair_checked:
+            return y
+        with torch.cuda.device(self.device):
+            if torch.cuda.is_current_stream_capturing():  # no timing inside a graph capture
+                return y
+        best = None
+        for attempt in range(PAIR_TRIES):
+            pass_ms, round_ms = self._pair_timer(x, y, plan, steps, self.P)
+            self.pair_probes.append({"attempt": attempt, "pass_ms": pass_ms, "round_ms": round_ms,
+                                     "ratio": pass_ms / round_ms if round_ms > 0 else float("inf")})
+            if best is None or pass_ms < best[0]:
+                best = (pass_ms, y)
+            if pass_ms <= PAIR_RATIO * round_ms or attempt + 1 == PAIR_TRIES:
+                break
+            y = device_matrix(self.n, self.ld, self.device)  # a fresh allocation for the destination
+        y = best[1]
+        self._buf["y"] = y
+        self._pair_checked.add((x.data_ptr(), y.data_ptr()))
+        return y
 
     # ------------------------------------------------------------------ primal / dual
     def local_step(self, lr: float, momentum: float, first_step: bool, theta: Optional[torch.Tensor] = None,

@@ -133,3 +133,47 @@ def test_bank_maps_large_state_when_asked(gpu, monkeypatch):
     monkeypatch.setenv("DOL_BANK_ALLOC", "torch")
     B.AgentBank(64, 8192, gpu).buffer("x")
     assert len(made) == 1
+
+
+def test_fused_pass_destination_check_replaces_a_slow_pair(gpu, monkeypatch):
+    """AgentBank.mix's destination check (r05): before a fused
+    ring pass first writes "y" from a given "x", the pair is timed; a pair whose
+    pass is slower than PAIR_RATIO x one ring round gets a fresh destination
+    (its contents are dead).  Injected timer: the first pair reads slow, every
+    later one fast -> exactly one replacement, both directions checked once, and
+    the mixed state bit-identical to a bank without the check (and the oracle)."""
+    from dolhip import graph as G
+    monkeypatch.setattr(B, "PAIR_PROBE_MIN_BYTES", 0)
+    n, P = 96, 1000
+    rng = np.random.default_rng(31)
+    X0 = rng.standard_normal((n, P)).astype(np.float32)
+    plan = G.MixingPlan(G.communication_csr("circle", "stochastic", n)[0], gpu)
+    assert plan.kind == "ring"
+    calls = []
+
+    def timer(x, y, plan_, steps, P_):
+        calls.append((x.data_ptr(), y.data_ptr(), steps))
+        return (2.0, 1.0) if len(calls) == 1 else (1.0, 1.0)
+
+    def run(check):
+        monkeypatch.setenv("DOL_BANK_PAIR_PROBE", "1" if check else "0")
+        bank = B.AgentBank(n, P, gpu)
+        bank._pair_timer = timer
+        bank.rows().copy_(torch.from_numpy(X0).to(gpu))
+        y_first = bank.buffer("y").data_ptr()
+        for _ in range(3):
+            bank.mix(plan, steps=5)
+        torch.cuda.synchronize()
+        return bank, y_first, bank.rows().cpu().numpy()
+
+    bank, y_first, got = run(True)
+    assert len(calls) == 3  # pair 1 slow -> replaced and re-timed; the swapped pair once; then cached
+    assert calls[0][1] == y_first and calls[1][1] != y_first and calls[0][0] == calls[1][0]
+    assert [p["attempt"] for p in bank.pair_probes] == [0, 1, 0]
+    _, _, plain = run(False)
+    assert bits_equal(got, plain)
+    want = X0
+    wp, wn = (t.cpu().numpy() for t in (plan.w_prev, plan.w_next))
+    for _ in range(15):
+        want = oracle.mix_ring(want, wp, wn)
+    assert bits_equal(got, want)
