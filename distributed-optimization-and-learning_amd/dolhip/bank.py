@@ -328,18 +328,25 @@ class AgentBank:
         with torch.cuda.device(self.device):
             if torch.cuda.is_current_stream_capturing():  # no timing inside a graph capture
                 return y
-        best = None
-        for attempt in range(PAIR_TRIES):
-            pass_ms, round_ms = self._pair_timer(x, y, plan, steps, self.P)
-            self.pair_probes.append({"attempt": attempt, "pass_ms": pass_ms, "round_ms": round_ms,
-                                     "ratio": pass_ms / round_ms if round_ms > 0 else float("inf")})
-            if best is None or pass_ms < best[0]:
-                best = (pass_ms, y)
-            if pass_ms <= PAIR_RATIO * round_ms or attempt + 1 == PAIR_TRIES:
-                break
-            y = device_matrix(self.n, self.ld, self.device)  # a fresh allocation for the destination
-        y = best[1]
-        self._buf["y"] = y
+        best = (float("inf"), y)
+        del self._buf["y"]  # held in y / best only: a losing candidate is freed when replaced
+        try:
+            for attempt in range(PAIR_TRIES):
+                pass_ms, round_ms = self._pair_timer(x, y, plan, steps, self.P)
+                self.pair_probes.append({"attempt": attempt, "pass_ms": pass_ms, "round_ms": round_ms,
+                                         "ratio": pass_ms / round_ms if round_ms > 0 else float("inf")})
+                if pass_ms < best[0]:
+                    best = (pass_ms, y)
+                if pass_ms <= PAIR_RATIO * round_ms or attempt + 1 == PAIR_TRIES:
+                    break
+                try:  # a fresh allocation for the destination; no memory for one: keep the best so far
+                    y = device_matrix(self.n, self.ld, self.device)
+                except RuntimeError:  # torch's OOM and DolNativeError alike
+                    self.pair_probes[-1]["realloc_failed"] = True
+                    break
+        finally:
+            y = best[1]
+            self._buf["y"] = y
         self._pair_checked.add((x.data_ptr(), y.data_ptr()))
         return y
 
