@@ -435,12 +435,15 @@ def random_regular_pm_round(device, X, Y, N: int, P: int, reps: int = 10):
     ms = _events_ms(lambda: ops.mix_csr_pm(XT, YT, rp, col, val), reps)
     entry = ops.pm_stage_order_choice(XT, YT, N, P=P)
     ms_default = _events_ms(lambda: ops.mix_csr_pm(XT, YT, rp, col, val, nseg=0), reps)
+    # the same call in the other direction (a parameter-major DGD alternates XT / YT; DESIGN §4.4:
+    # some pairs of allocations are slower one way)
+    ms_reverse = _events_ms(lambda: ops.mix_csr_pm(YT, XT, rp, col, val), reps)
     gbps = 2 * N * P * 4 / (ms / 1e3) / 1e9
     return {"agents": N, "params": P, "degree": 4, "ms_per_round": ms, "rounds_per_s": 1e3 / ms, "GBps": gbps,
             "frac": gbps / HBM_PEAK_GBPS, "kernel": "csr_pm_kernel (parameter-major bank)",
             "stage_order": entry["choice"] if entry else 0,
             "stage_order_ms": {str(k): v for k, v in (entry["ms"] if entry else {}).items()},
-            "default_ms_per_round": ms_default,
+            "default_ms_per_round": ms_default, "reverse_direction_ms": ms_reverse,
             "what": "random 4-regular W mix on the parameter-major bank, bit-identical to the reference consensus"}
 
 
