@@ -257,9 +257,11 @@ def primal_dual_round(N: int, P: int, world: int, rank: int, device, steps: int,
     from dolhip.synthetic import SeparableADMM
     prob = SeparableADMM(N, P, rho=0.1, lr=0.1, momentum=0.5, local_steps=local_steps, frac=1.0, seed=2028,
                          device=device, mean="fast")
+    fused = prob.fused  # client round + this rank's ordered sum in one pass (dol_admm_ls_round_mean_f32)
+    names = ("round_mean",) if fused else ("client_round", "mean")
     ev = {k: [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
-          for k in ("client_round", "mean")}
-    rnd, osum = ops.admm_ls_round, ops.ordered_sum
+          for k in names}
+    rnd, rnd_mean = ops.admm_ls_round, prob._round_mean
     state = {"k": None}
 
     def timed_round(*a, **kw):
@@ -271,7 +273,17 @@ def primal_dual_round(N: int, P: int, world: int, rank: int, device, steps: int,
             ev["client_round"][k][1].record()
             ev["mean"][k][0].record()
 
+    def timed_round_mean(*a, **kw):
+        k = state["k"]
+        if k is not None:
+            ev["round_mean"][k][0].record()
+        out = rnd_mean(*a, **kw)
+        if k is not None:
+            ev["round_mean"][k][1].record()
+        return out
+
     prob._round = timed_round
+    prob._round_mean = timed_round_mean
     prob.round()  # warm-up (first momentum step)
     torch.cuda.synchronize(device)
     if world > 1:
@@ -280,7 +292,8 @@ def primal_dual_round(N: int, P: int, world: int, rank: int, device, steps: int,
     for k in range(steps):
         state["k"] = k
         prob.round()
-        ev["mean"][k][1].record()
+        if not fused:
+            ev["mean"][k][1].record()
     torch.cuda.synchronize(device)
     if world > 1:
         dist.barrier()
@@ -291,12 +304,36 @@ def primal_dual_round(N: int, P: int, world: int, rank: int, device, steps: int,
     n = prob.n
     row_bytes = n * P * 4
     # compulsory bytes: client round reads t, alpha, buf and writes w, alpha, buf; the mean reads w, writes theta
-    alg = {"client_round": 6 * row_bytes, "mean": row_bytes + P * 4}
+    # (fused: the new w rows are summed in registers, theta read once and written once)
+    alg = ({"round_mean": 6 * row_bytes + 2 * P * 4} if fused else
+           {"client_round": 6 * row_bytes, "mean": row_bytes + P * 4})
     kern = {}
     for nm in alg:
         ms = float(np.mean([a.elapsed_time(b) for a, b in ev[nm]]))
         kern[nm] = {"ms": ms, "GBps": alg[nm] / (ms / 1e3) / 1e9, "frac": alg[nm] / (ms / 1e3) / 1e9 / HBM_PEAK_GBPS,
                     "algorithmic_bytes": alg[nm]}
+    two_kernel = None
+    if fused:
+        # the same round on the two-kernel path (client round, then the ordered
+        # sum re-reading the rows), same buffers, for comparison
+        state["k"] = None
+        prob.fused = False
+        prob.round()
+        torch.cuda.synchronize(device)
+        if world > 1:
+            dist.barrier()
+        t1 = time.perf_counter()
+        for _ in range(3):
+            prob.round()
+        torch.cuda.synchronize(device)
+        if world > 1:
+            dist.barrier()
+        tk = torch.tensor([(time.perf_counter() - t1) / 3], dtype=torch.float64, device=device)
+        if world > 1:
+            dist.all_reduce(tk, op=dist.ReduceOp.MAX)
+        prob.fused = True
+        two_kernel = {"ms_per_round": float(tk.item()) * 1e3,
+                      "what": "dol_admm_ls_round_f32 + ordered sum (the mean re-reads the new rows), host-timed"}
     exact = None
     if world > 1:
         # the bit-exact server mean across ranks (DEC/servers.py:42-48's order):
@@ -320,10 +357,12 @@ def primal_dual_round(N: int, P: int, world: int, rank: int, device, steps: int,
                  "what": "global_mean_exact: all_to_all of the sampled rows to column blocks + ordered sum + all_gather"}
     hist = prob.history
     out = {"rounds_per_s": steps / el, "ms_per_round": el / steps * 1e3, "agents": N, "params": P,
-           "local_steps": local_steps, "kernels": kern, "exact_mean": exact,
+           "local_steps": local_steps, "kernels": kern, "fused_round_mean": fused, "two_kernel_round": two_kernel,
+           "exact_mean": exact,
            "primal_resid_sq_last": hist[-1]["primal_resid_sq"], "dual_sq_last": hist[-1]["dual_sq"],
            "what": "FedADMM least-squares round over all agents: fused client round (w = theta, %d momentum-SGD "
-                   "steps with the ADMM term, dual ascent) + all_reduce mean" % local_steps}
+                   "steps with the ADMM term, dual ascent) with this rank's ordered sum of the new rows in the "
+                   "same pass, + all_reduce mean at world > 1" % local_steps}
     del prob
     torch.cuda.empty_cache()
     return out

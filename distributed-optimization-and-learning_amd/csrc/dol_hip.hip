@@ -989,8 +989,49 @@ __device__ __forceinline__ void admm_ls_lane(float& w, float& b, float& a, float
   }
   const float dl = w - th;
   a = a + rho * dl;
-  rw += double(dl) * double(dl);
-  ra += double(a) * double(a);
+  // the product of two floats is exact in double, so fma == the reference's
+  // separately rounded rw + d*d, one instruction fewer
+  rw = __builtin_fma(double(dl), double(dl), rw);
+  ra = __builtin_fma(double(a), double(a), ra);
+}
+
+// The same lane on two columns at once: packed fp32 (v_pk_add / v_pk_mul /
+// v_pk_fma_f32 on gfx950, each an IEEE operation per half), same rounding per
+// element as admm_ls_lane.  At 10 local steps the round runs ~70 fp32 ops per
+// element: unpacked that is ~60 % of the HBM time in VALU issue.
+typedef float f2 __attribute__((ext_vector_type(2)));
+template <bool MOM>
+__device__ __forceinline__ void admm_ls_lane2(f2& w, f2& b, f2& a, f2 t, f2 th, float rho, float neg_lr, float mom,
+                                              int steps, bool first, double& rw, double& ra) {
+  const f2 rho2 = {rho, rho}, nlr2 = {neg_lr, neg_lr}, mom2 = {mom, mom};
+  w = th;
+  for (int k = 0; k < steps; ++k) {
+    const f2 g = w - t;
+    const f2 gg = g + (a + rho2 * (w - th));
+    f2 d = gg;
+    if constexpr (MOM) {
+      b = (first && k == 0) ? gg : b * mom2 + gg;
+      d = b;
+    }
+    w = __builtin_elementwise_fma(nlr2, d, w);
+  }
+  const f2 dl = w - th;
+  a = a + rho2 * dl;
+  rw = __builtin_fma(double(dl.x), double(dl.x), rw);
+  rw = __builtin_fma(double(dl.y), double(dl.y), rw);
+  ra = __builtin_fma(double(a.x), double(a.x), ra);
+  ra = __builtin_fma(double(a.y), double(a.y), ra);
+}
+// f4 = two packed halves
+template <bool MOM>
+__device__ __forceinline__ void admm_ls_lane4(f4& w, f4& b, f4& a, f4 t, f4 th, float rho, float neg_lr, float mom,
+                                              int steps, bool first, double& rw, double& ra) {
+  f2 w0, w1, b0 = b.xy, b1 = b.zw, a0 = a.xy, a1 = a.zw;
+  admm_ls_lane2<MOM>(w0, b0, a0, t.xy, th.xy, rho, neg_lr, mom, steps, first, rw, ra);
+  admm_ls_lane2<MOM>(w1, b1, a1, t.zw, th.zw, rho, neg_lr, mom, steps, first, rw, ra);
+  w = f4{w0.x, w0.y, w1.x, w1.y};
+  b = f4{b0.x, b0.y, b1.x, b1.y};
+  a = f4{a0.x, a0.y, a1.x, a1.y};
 }
 
 template <bool VEC, bool MOM, bool RESID>
@@ -1032,14 +1073,7 @@ __global__ __launch_bounds__(kThreads) void admm_ls_round_kernel(
         f4 a = __builtin_nontemporal_load(reinterpret_cast<const f4*>(ar) + c);
         f4 b = MOM ? __builtin_nontemporal_load(reinterpret_cast<const f4*>(br) + c) : f4{0.f, 0.f, 0.f, 0.f};
         f4 w;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          float wj, bj = b[j], aj = a[j];
-          admm_ls_lane<MOM>(wj, bj, aj, t[j], th[j], rho, neg_lr, mom, steps, fst, rw, ra);
-          w[j] = wj;
-          b[j] = bj;
-          a[j] = aj;
-        }
+        admm_ls_lane4<MOM>(w, b, a, t, th, rho, neg_lr, mom, steps, fst, rw, ra);
         __builtin_nontemporal_store(w, reinterpret_cast<f4*>(wr) + c);
         __builtin_nontemporal_store(a, reinterpret_cast<f4*>(ar) + c);
         if constexpr (MOM) __builtin_nontemporal_store(b, reinterpret_cast<f4*>(br) + c);
@@ -1097,6 +1131,148 @@ __global__ __launch_bounds__(kThreads) void ordered_sum_kernel(
   for (; k < m; ++k) acc = vadd(acc, wb[int64_t(order[k]) * ldv]);
   if (do_div) acc = vdiv(acc, scale);
   *(reinterpret_cast<V*>(out + c_off) + c) = acc;
+}
+
+// ----------------------------------------------------------------------------
+// The FedADMM client round fused with the server's ordered mean (one round of
+// DEC/servers.py:50-81 on least squares: every sampled client's
+// update_weights, DEC/clients.py:36-53, then average_weights, :42-48).
+// Column-strip major: each lane owns one V-column and walks the m sampled
+// agents in the given order, running admm_ls_lane on (agent, column) and
+// chaining acc = w(first) ; acc = fl(acc + w) — the ordered_sum_kernel's
+// association, so theta_next is the same bits as admm_ls_round_kernel +
+// ordered_sum_kernel — while the w rows are still in registers: the separate
+// mean read every sampled row back from HBM (34 GB at 8192 x 2^20, 15 % of the
+// round's bytes).  theta is read once per lane, not once per (agent, column).
+// The next agent group's t / alpha / buf loads are issued before the current
+// group's steps (kRoundPF agents in flight per lane).
+// RESID: fp64 per-lane sums over the agents of (w - theta)^2 and alpha^2, a
+// fixed block tree, one partial per block; resid_reduce_kernel folds the
+// blocks in a fixed order (the round's totals, not per agent).
+// ----------------------------------------------------------------------------
+constexpr int kRoundPF = 3;
+
+template <bool MOM>
+__device__ __forceinline__ void admm_ls_lane_v(float& w, float& b, float& a, float t, float th, float rho, float neg_lr,
+                                               float mom, int steps, bool first, double& rw, double& ra) {
+  admm_ls_lane<MOM>(w, b, a, t, th, rho, neg_lr, mom, steps, first, rw, ra);
+}
+// packed (measured at 8192 x 2^20, 10 steps: 34.6-35.1 ms vs 36.0-36.5 with
+// the per-element scalar form, profiles/r05zw_admm_round_ab.jsonl)
+template <bool MOM>
+__device__ __forceinline__ void admm_ls_lane_v(f4& w, f4& b, f4& a, f4 t, f4 th, float rho, float neg_lr, float mom,
+                                               int steps, bool first, double& rw, double& ra) {
+  admm_ls_lane4<MOM>(w, b, a, t, th, rho, neg_lr, mom, steps, first, rw, ra);
+}
+__device__ __forceinline__ float ldnt(const float* p) { return __builtin_nontemporal_load(p); }
+__device__ __forceinline__ f4 ldnt(const f4* p) { return __builtin_nontemporal_load(p); }
+// nontemporal buffer store of lane value v at byte offset voff of the row at
+// base (row-uniform resource); voff = kOOB drops it (still issued and counted)
+__device__ __forceinline__ void st_row(float v, float* base, int64_t nbytes, uint32_t voff) {
+  const rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, static_cast<int>(nbytes), 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, voff, 0, 2);
+}
+__device__ __forceinline__ void st_row(f4 v, float* base, int64_t nbytes, uint32_t voff) {
+  const rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, static_cast<int>(nbytes), 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), rs, voff, 0, 2);
+}
+
+template <int NT>
+__device__ __forceinline__ double block_sum_f64_nt(double v, double* smem) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) smem[wid] = v;
+  __syncthreads();
+  double s = 0.0;
+  if (threadIdx.x == 0) {
+    for (int i = 0; i < NT / 64; ++i) s += smem[i];
+  }
+  return s;
+}
+
+template <typename V, bool MOM, bool RESID, int NT>
+__global__ __launch_bounds__(NT) void admm_ls_round_mean_kernel(
+    float* __restrict__ W, int64_t ldw, float* __restrict__ B, int64_t ldb, float* __restrict__ A, int64_t lda,
+    const float* __restrict__ T, int64_t ldt, const float* __restrict__ theta, const int32_t* __restrict__ agents,
+    const int32_t* __restrict__ first, int m, int64_t c_off, int64_t ncols_v, float rho, float neg_lr, float mom,
+    int steps, float* __restrict__ out, float scale, int do_div, double* __restrict__ partial, int64_t part_off,
+    int64_t part_stride) {
+  __shared__ double smem[NT / 64];
+  const int64_t c = int64_t(blockIdx.x) * NT + threadIdx.x;
+  const bool live = c < ncols_v;
+  if (!RESID && !live) return;
+  // dead lanes (RESID only) read the last real column and compute on it; their
+  // stores are buffer stores pointed out of range (dropped, still counted, so
+  // every lane issues the same memory ops and the loop's vmcnt waits stay
+  // exact) and their residual terms are dropped
+  const int64_t cc = live ? c : ncols_v - 1;
+  const uint32_t voff = live ? uint32_t(c) * uint32_t(sizeof(V)) : kOOB;
+  auto st = [&](V v, float* base, int64_t ld, int64_t row) {
+    st_row(v, base + row * ld + c_off, std::min<int64_t>((ld - c_off) * 4, 0x7ffffff0), voff);
+  };
+  auto cptr = [&](const float* base, int64_t ld, int64_t row) {
+    return reinterpret_cast<const V*>(base + row * ld + c_off) + cc;
+  };
+  auto row_of = [&](int k) -> int64_t {  // agent k's row; k past m: the last agent's (a harmless re-read)
+    k = min(k, m - 1);
+    return agents ? agents[k] : k;
+  };
+  const V th = *cptr(theta, 0, 0);
+  V acc = vzero(th);
+  double rw = 0.0, ra = 0.0;
+  struct Grp {
+    V t[kRoundPF], a[kRoundPF], b[kRoundPF];
+    int64_t row[kRoundPF];
+  };
+  auto load = [&](Grp& g, int k0) {  // agents k0 .. k0 + kRoundPF - 1, unconditionally (rows clamped)
+#pragma unroll
+    for (int u = 0; u < kRoundPF; ++u) {
+      g.row[u] = row_of(k0 + u);
+      g.t[u] = ldnt(cptr(T, ldt, g.row[u]));
+      g.a[u] = ldnt(cptr(A, lda, g.row[u]));
+      if constexpr (MOM) g.b[u] = ldnt(cptr(B, ldb, g.row[u]));
+    }
+  };
+  auto run = [&](Grp& g, int u, int k) {  // agent k = group slot u: its steps, stores, and the chain
+    const bool fst = first ? first[k] != 0 : false;
+    V w, bu = MOM ? g.b[u] : vzero(th), au = g.a[u];
+    double rwu = 0.0, rau = 0.0;
+    admm_ls_lane_v<MOM>(w, bu, au, g.t[u], th, rho, neg_lr, mom, steps, fst, rwu, rau);
+    st(w, W, ldw, g.row[u]);
+    st(au, A, lda, g.row[u]);
+    if constexpr (MOM) st(bu, B, ldb, g.row[u]);
+    rw += live ? rwu : 0.0;
+    ra += live ? rau : 0.0;
+    acc = k == 0 ? w : vadd(acc, w);
+  };
+  const int ng = (m + kRoundPF - 1) / kRoundPF;  // groups; all but the last are full
+  Grp nxt, cur;
+  load(nxt, 0);
+  for (int gi = 0; gi + 1 < ng; ++gi) {  // straight-line body: the same memory ops every trip
+    cur = nxt;
+    load(nxt, (gi + 1) * kRoundPF);      // the next group's loads fly during this group's steps
+#pragma unroll
+    for (int u = 0; u < kRoundPF; ++u) run(cur, u, gi * kRoundPF + u);
+  }
+#pragma unroll
+  for (int u = 0; u < kRoundPF; ++u) {   // the last group (maybe partial)
+    const int k = (ng - 1) * kRoundPF + u;
+    if (k < m) run(nxt, u, k);
+  }
+  if (live) {
+    if (do_div) acc = vdiv(acc, scale);
+    *(reinterpret_cast<V*>(out + c_off) + c) = acc;
+  }
+  if constexpr (RESID) {
+    const double sw = block_sum_f64_nt<NT>(rw, smem);
+    __syncthreads();
+    const double sa = block_sum_f64_nt<NT>(ra, smem);
+    if (threadIdx.x == 0) {
+      partial[part_off + blockIdx.x] = sw;
+      partial[part_stride + part_off + blockIdx.x] = sa;
+    }
+  }
 }
 
 // Calibration copy: each block streams one contiguous 16 KiB chunk (4 x f4
@@ -2030,6 +2206,65 @@ int dol_admm_ls_round_f32(float* w, int64_t ldw, float* buf, int64_t ldb, float*
     hipLaunchKernelGGL(resid_reduce_kernel, dim3(m), dim3(kThreads), 0, s, partial + int64_t(m) * chunks, chunks,
                        alpha_sq);
   }
+  return check_launch(nm);
+}
+
+int64_t dol_admm_ls_round_mean_workspace_bytes(int64_t P) {
+  if (P <= 0 || P > dol::kMaxDim) return 0;
+  return 2 * (cdiv(P, kThreads) + 1) * int64_t(sizeof(double));  // [2][blocks]: (w - theta)^2, alpha^2
+}
+
+int dol_admm_ls_round_mean_f32(float* w, int64_t ldw, float* buf, int64_t ldb, float* alpha, int64_t lda,
+                               const float* target, int64_t ldt, const float* theta, const int32_t* agents,
+                               const int32_t* first, int32_t m, int64_t P, float rho, float lr, float momentum,
+                               int32_t local_steps, float* theta_out, float scale, double* resid_total, void* work,
+                               hipStream_t s) {
+  DOL_DIMS_OK("dol_admm_ls_round_mean_f32", ldw, ldb, lda, ldt, P);
+  const char* nm = "dol_admm_ls_round_mean_f32";
+  if (m < 1) return fail(DOL_EINVAL, "%s: m must be >= 1 (the average indexes w[0])", nm);
+  if (P < 0 || local_steps < 0) return fail(DOL_EINVAL, "%s: negative size", nm);
+  if (!(scale > 0.0f)) return fail(DOL_EINVAL, "%s: scale must be > 0", nm);
+  const bool mom = momentum != 0.0f;
+  if (P > 0 && (!w || !alpha || !target || !theta || !theta_out || (mom && !buf)))
+    return fail(DOL_EINVAL, "%s: null pointer", nm);
+  if (theta_out == w || theta_out == alpha || theta_out == target || (mom && theta_out == buf))
+    return fail(DOL_EINVAL, "%s: theta_out aliases the rows", nm);
+  if (resid_total && !work && P > 0) return fail(DOL_EINVAL, "%s: resid_total needs a workspace", nm);
+  if (ldw < P || lda < P || ldt < P || (mom && ldb < P)) return fail(DOL_EINVAL, "%s: ld < P", nm);
+  if (P > (int64_t(1) << 29) - 16) return fail(DOL_EINVAL, "%s: P >= 2^29 (row offsets are 32-bit buffer offsets)", nm);
+  if (P == 0) {
+    if (resid_total) (void)hipMemsetAsync(resid_total, 0, 2 * sizeof(double), s);
+    return check_launch(nm);
+  }
+  const bool vec_ok = row_vec_ok(w, ldw) && row_vec_ok(alpha, lda) && row_vec_ok(target, ldt) &&
+                      row_vec_ok(theta, 0) && row_vec_ok(theta_out, 0) && (!mom || row_vec_ok(buf, ldb));
+  const ColSplit cs = split_cols(P, vec_ok);
+  // column strip per workgroup: 1024 lanes (16 KiB of each row per workgroup,
+  // one workgroup per CU at 2^20 columns) unless DOL_ADMM_ROUND_THREADS=256
+  static const bool wide = env_int("DOL_ADMM_ROUND_THREADS", 1024) != 256;
+  const int64_t nt = wide ? 1024 : 256;
+  const int64_t nb4 = cdiv(cs.n4, nt), nbt = cdiv(cs.tail, nt);
+  const int64_t nb = nb4 + nbt;
+  double* partial = static_cast<double*>(work);
+  const int do_div = scale != 1.0f;
+  auto go = [&](auto vt, auto mc, auto rc, int64_t c_off, int64_t ncols, int64_t blocks, int64_t part_off) {
+    using V = decltype(vt);
+    constexpr bool M = decltype(mc)::value, R = decltype(rc)::value;
+    auto k = wide ? admm_ls_round_mean_kernel<V, M, R, 1024> : admm_ls_round_mean_kernel<V, M, R, 256>;
+    hipLaunchKernelGGL(k, dim3(static_cast<unsigned>(blocks)), dim3(wide ? 1024 : 256), 0, s, w, ldw, buf, ldb, alpha,
+                       lda, target, ldt, theta, agents, first, m, c_off, ncols, rho, -lr, momentum, local_steps,
+                       theta_out, scale, do_div, partial, part_off, nb);
+  };
+  using std::integral_constant;
+  using Tb = integral_constant<bool, true>;
+  using Fb = integral_constant<bool, false>;
+  auto both = [&](auto vt, int64_t c_off, int64_t ncols, int64_t blocks, int64_t part_off) {
+    if (mom) { if (resid_total) go(vt, Tb{}, Tb{}, c_off, ncols, blocks, part_off); else go(vt, Tb{}, Fb{}, c_off, ncols, blocks, part_off); }
+    else { if (resid_total) go(vt, Fb{}, Tb{}, c_off, ncols, blocks, part_off); else go(vt, Fb{}, Fb{}, c_off, ncols, blocks, part_off); }
+  };
+  if (cs.n4 > 0) both(f4{}, 0, cs.n4, nb4, 0);
+  if (cs.tail > 0) both(float{}, cs.n4 * 4, cs.tail, nbt, nb4);
+  if (resid_total) hipLaunchKernelGGL(resid_reduce_kernel, dim3(2), dim3(kThreads), 0, s, partial, nb, resid_total);
   return check_launch(nm);
 }
 

@@ -49,6 +49,9 @@ SIGNATURES = {
     "dol_admm_ls_round_f32": [_ptr, _i64, _ptr, _i64, _ptr, _i64, _ptr, _i64, _ptr, _ptr, _ptr, _i32, _i64, _f32, _f32,
                               _f32, _i32, _ptr, _ptr, _ptr, _ptr],
     "dol_admm_ls_round_workspace_bytes": [_i32, _i64],
+    "dol_admm_ls_round_mean_f32": [_ptr, _i64, _ptr, _i64, _ptr, _i64, _ptr, _i64, _ptr, _ptr, _ptr, _i32, _i64, _f32,
+                                   _f32, _f32, _i32, _ptr, _f32, _ptr, _ptr, _ptr],
+    "dol_admm_ls_round_mean_workspace_bytes": [_i64],
     "dol_ordered_mean_f32": [_ptr, _i64, _ptr, _i32, _i64, _ptr, _ptr],
     "dol_ordered_sum_f32": [_ptr, _i64, _ptr, _i32, _i64, _ptr, _ptr, _f32, _ptr],
     "dol_stream_copy_f32": [_ptr, _ptr, _i64, _ptr],
@@ -84,6 +87,7 @@ SIGNATURES = {
 }
 _RESTYPES = {"dol_last_error": ctypes.c_char_p, "dol_admm_dual_workspace_bytes": ctypes.c_int64,
              "dol_admm_ls_round_workspace_bytes": ctypes.c_int64,
+             "dol_admm_ls_round_mean_workspace_bytes": ctypes.c_int64,
              "dol_mlp_step_lds_bytes": ctypes.c_int64, "dol_mlp_step_workspace_bytes": ctypes.c_int64,
              "dol_mix_dense_split3_workspace_bytes": ctypes.c_int64, "dol_csr_slab_hdr_len": ctypes.c_int64,
              "dol_csr_slab_ent_len": ctypes.c_int64}

@@ -872,6 +872,65 @@ def admm_ls_round(w: torch.Tensor, alpha: torch.Tensor, target: torch.Tensor, th
                  _ptr(work) if resid_sq is not None else None, _stream(w))
 
 
+def admm_ls_round_mean(w: torch.Tensor, alpha: torch.Tensor, target: torch.Tensor, theta: torch.Tensor,
+                       agents: Optional[torch.Tensor] = None, first: Optional[torch.Tensor] = None,
+                       buf: Optional[torch.Tensor] = None, rho: float = 0.1, lr: float = 0.1, momentum: float = 0.0,
+                       local_steps: int = 1, out: Optional[torch.Tensor] = None, scale: Optional[float] = None,
+                       resid_total: Optional[torch.Tensor] = None, work: Optional[torch.Tensor] = None,
+                       P: Optional[int] = None) -> torch.Tensor:
+    """admm_ls_round + the server's ordered average in ONE pass
+    (dol_admm_ls_round_mean_f32): the rows come out as admm_ls_round leaves
+    them and `out` = ordered_sum(w, agents, scale=scale) of the new rows, the
+    same bits, without reading w back.  scale None = m (the mean,
+    DEC/servers.py:42-48); 1.0 = the raw ordered sum.  agents: DISTINCT rows in
+    the sampled order (None = 0..n-1).  resid_total: float64 [2] output, the
+    round's sums over the agents of ||w - theta||^2 and ||alpha||^2.
+    Reference: DEC/servers.py:50-81 (Server.run's round) on least squares."""
+    P = w.shape[1] if P is None else P
+    ldw = _check_rows("w", w, P)
+    lda = _check_rows("alpha", alpha, P)
+    ldt = _check_rows("target", target, P)
+    n = w.shape[0]
+    if alpha.shape[0] < n or target.shape[0] < n:
+        raise ValueError("alpha/target have fewer rows than w")
+    _check_vec("theta", theta, P, w.device)
+    if int(local_steps) < 0:
+        raise ValueError("local_steps must be >= 0")
+    ldb = 0
+    if momentum != 0.0:
+        if buf is None:
+            raise ValueError("momentum != 0 needs buf")
+        ldb = _check_rows("buf", buf, P)
+        if buf.shape[0] < n:
+            raise ValueError("buf has fewer rows than w")
+    m = n
+    if agents is not None:
+        _check_order(agents, w.device, n)
+        m = agents.numel()
+    if m < 1:
+        raise ValueError("admm_ls_round_mean needs at least one agent (the average indexes w[0])")
+    if first is not None and (first.device != w.device or first.dtype != torch.int32 or not first.is_contiguous()
+                              or first.numel() < m):
+        raise ValueError(f"first: expected contiguous int32 [{m}] on {w.device}")
+    if out is None:
+        out = torch.empty(P, dtype=torch.float32, device=w.device)
+    _check_vec("out", out, P, w.device)
+    if resid_total is not None:
+        if (resid_total.dtype != torch.float64 or resid_total.numel() < 2 or resid_total.device != w.device
+                or not resid_total.is_contiguous()):
+            raise ValueError(f"resid_total: expected contiguous float64 [2] on {w.device}")
+        need = int(_native.lib().dol_admm_ls_round_mean_workspace_bytes(int(P)))
+        if work is None:
+            work = _workspace(w.device, need)
+        elif work.device != w.device or work.numel() * work.element_size() < need:
+            raise ValueError(f"work: need {need} bytes on {w.device}")
+    _native.call("dol_admm_ls_round_mean_f32", w.data_ptr(), ldw, _ptr(buf) if ldb else None, ldb, alpha.data_ptr(),
+                 lda, target.data_ptr(), ldt, theta.data_ptr(), _ptr(agents), _ptr(first), m, P, float(rho), float(lr),
+                 float(momentum), int(local_steps), out.data_ptr(), float(m if scale is None else scale),
+                 _ptr(resid_total), _ptr(work) if resid_total is not None else None, _stream(w))
+    return out
+
+
 def _check_order(order: torch.Tensor, device, n_rows: int) -> None:
     if order.device != device or order.dtype != torch.int32 or not order.is_contiguous():
         raise ValueError("order: expected contiguous int32 on the rows' device")

@@ -587,6 +587,14 @@ def global_mean(local_rows: torch.Tensor, local_order: Sequence[int], m_total: i
         ordered_sum(local_rows, idx, out=out, P=P)
     else:
         out.zero_()
+    return global_mean_finish(out, m_total, P, group=group, ordered_sum=ordered_sum)
+
+
+def global_mean_finish(out: torch.Tensor, m_total: int, P: int, group=None, ordered_sum=None) -> torch.Tensor:
+    """The rest of `global_mean` once `out` holds this rank's local ordered
+    sum (zeros without sampled rows): all_reduce(SUM), then / m in place."""
+    ordered_sum = ordered_sum if ordered_sum is not None else ops.ordered_sum
+    device = out.device
     if dist.is_initialized() and dist.get_world_size(group) > 1:
         if out.device.type == "cuda" and dist.get_backend(group) == "gloo":
             host = out.cpu()

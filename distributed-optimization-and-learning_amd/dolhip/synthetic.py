@@ -115,7 +115,7 @@ class SeparableADMM:
 
     def __init__(self, n_agents: int, P: int, rho: float = 0.1, lr: float = 0.1, momentum: float = 0.5,
                  local_steps: int = 1, frac: float = 1.0, seed: int = 2028, device=None, mean: str = "exact",
-                 group=None, metrics: bool = True, round_fn=None, ordered_sum=None):
+                 group=None, metrics: bool = True, round_fn=None, ordered_sum=None, fused: Optional[bool] = None):
         import numpy as np
         import torch.distributed as dist
 
@@ -134,6 +134,16 @@ class SeparableADMM:
         self.device = torch.device(device) if device is not None else torch.device("cuda")
         self._round = round_fn if round_fn is not None else ops.admm_ls_round
         self._osum = ordered_sum if ordered_sum is not None else ops.ordered_sum
+        # the client round and the mean in one pass (dol_admm_ls_round_mean_f32)
+        # wherever the mean is this rank's ordered sum of its own rows: one
+        # process, or the 'fast' mean's local part; off with injected checkers
+        # or DOL_ADMM_FUSED_MEAN=0
+        import os
+        if fused is None:
+            fused = os.environ.get("DOL_ADMM_FUSED_MEAN", "1") != "0"
+        self.fused = bool(fused) and round_fn is None and ordered_sum is None and \
+            (self.world == 1 or mean == "fast")
+        self._round_mean = ops.admm_ls_round_mean
         self._parallel = parallel
         self.rs = np.random.RandomState(seed)  # the reference's np.random.choice stream (setup_seed)
         ld = row_stride(self.P)
@@ -168,6 +178,8 @@ class SeparableADMM:
         dev = self.device
         ml = len(local)
         rw = ra = None
+        if self.fused:
+            return self._fused_round(order, local)
         if ml:
             rows = torch.as_tensor(local, dtype=torch.int32, device=dev)
             first = None
@@ -194,6 +206,44 @@ class SeparableADMM:
             if ml:
                 s[0] = rw.sum()
                 s[1] = ra.sum()
+            if self.world > 1:
+                import torch.distributed as dist
+                if s.device.type == "cuda" and dist.get_backend(self.group) == "gloo":
+                    h = s.cpu()
+                    dist.all_reduce(h, group=self.group)
+                    s.copy_(h)
+                else:
+                    dist.all_reduce(s, group=self.group)
+            self._pending.append((self.rounds, s))
+        self.rounds += 1
+
+    def _fused_round(self, order, local) -> None:
+        """round() on dol_admm_ls_round_mean_f32: the client round and this
+        rank's ordered sum of its new rows in one pass (one process: the mean
+        itself, bit-identical to the two-kernel round; 'fast' mean: the local
+        sum, then all_reduce + / m).  The residual metrics come as the round's
+        totals (fp64, another fixed summation order than the per-agent path's:
+        equal to ~1e-15 relative)."""
+        dev = self.device
+        ml = len(local)
+        s = torch.zeros(2, dtype=torch.float64, device=dev)
+        if ml:
+            rows = torch.as_tensor(local, dtype=torch.int32, device=dev)
+            first = None
+            if self.mom is not None:
+                first = torch.as_tensor(~self.mom_started[local], dtype=torch.int32, device=dev)
+            self._round_mean(self.w, self.alpha, self.target, self.theta, agents=rows, first=first, buf=self.mom,
+                             rho=self.rho, lr=self.lr, momentum=self.mu, local_steps=self.local_steps,
+                             out=self._theta_next, scale=float(self.m) if self.world == 1 else 1.0,
+                             resid_total=s if self.metrics else None, P=self.P)
+            if self.mom is not None and self.local_steps > 0:
+                self.mom_started[local] = True
+        else:  # a rank without sampled rows ('fast' mean): contributes zeros
+            self._theta_next.zero_()
+        if self.world > 1:
+            self._parallel.global_mean_finish(self._theta_next, self.m, self.P, group=self.group)
+        self.theta, self._theta_next = self._theta_next, self.theta
+        if self.metrics:
             if self.world > 1:
                 import torch.distributed as dist
                 if s.device.type == "cuda" and dist.get_backend(self.group) == "gloo":

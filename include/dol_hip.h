@@ -386,6 +386,29 @@ int dol_admm_ls_round_f32(float* w, int64_t ldw, float* buf, int64_t ldb, float*
 int64_t dol_admm_ls_round_workspace_bytes(int32_t m, int64_t P);
 
 /*
+ * dol_admm_ls_round_f32 fused with the server's ordered average: the whole
+ * round of DEC/servers.py:50-81 (every sampled client's update_weights,
+ * DEC/clients.py:36-53, then average_weights, DEC/servers.py:42-48) in one
+ * pass.  w / buf / alpha rows come out bit-identical to dol_admm_ls_round_f32,
+ * and theta_out to dol_ordered_sum_f32(w, agents, m, P, NULL, theta_out,
+ * scale) on them (acc = w[agents[0]]; acc = fl(acc + w[agents[k]]); theta_out
+ * = fl(acc / scale) when scale != 1; scale = m is the mean, scale = 1 the raw
+ * sum that a multi-rank 'fast' mean all-reduces) — without reading the new w
+ * rows back.  agents: [m] DISTINCT rows in the sampled order (NULL: 0..m-1),
+ * m >= 1.  theta_out may alias theta (each column is read before it is
+ * written); it must not alias the rows.  resid_total (nullable, fp64 [2])
+ * receives the round's sums over the agents of ||w_k - theta||^2 and
+ * ||alpha_k||^2 (a fixed reduction order, deterministic, not per agent); it
+ * needs `work` of dol_admm_ls_round_mean_workspace_bytes(P) bytes.  P < 2^29.
+ */
+int dol_admm_ls_round_mean_f32(float* w, int64_t ldw, float* buf, int64_t ldb, float* alpha, int64_t lda,
+                               const float* target, int64_t ldt, const float* theta, const int32_t* agents,
+                               const int32_t* first, int32_t m, int64_t P, float rho, float lr, float momentum,
+                               int32_t local_steps, float* theta_out, float scale, double* resid_total, void* work,
+                               hipStream_t s);
+int64_t dol_admm_ls_round_mean_workspace_bytes(int64_t P);
+
+/*
  * Ordered uniform average, replacing Server.average_weights
  *   DEC/servers.py:42-48:  acc = w[order[0]]; acc = fl(acc + w[order[k]]) k=1..m-1;
  *                          theta = fl(acc / (float)m)

@@ -108,3 +108,19 @@ def test_split3_fxw_waits_are_counted(split_code_object):
     assert "vscnt" not in asm
     assert len(re.findall(r"global_load_lds_dwordx4", asm)) >= 10  # prologue groups 0 and 1 (+ the loop's)
     assert not re.search(r"global_load_dword[^x_]|global_load_dwordx[24]\b|buffer_load", asm), "unexpected vector loads"
+
+
+def test_admm_round_mean_is_packed_and_counted(code_object):
+    """The one-pass FedADMM round + mean (admm_ls_round_mean_kernel, f4
+    columns): packed fp32 steps (v_pk_fma_f32 for the SGD update), row stores
+    as buffer stores (dead lanes dropped out of range, so every lane issues
+    the same memory ops) and counted vmcnt waits inside the agent loop -- not
+    only full drains."""
+    ks = [k for k in _kernels(code_object, "admm_ls_round_mean_kernel") if "Dv4_f" in k]
+    assert ks, "no f4 admm_ls_round_mean_kernel instantiations"
+    for k in ks:
+        asm = _disasm(code_object, k)
+        assert "v_pk_fma_f32" in asm, k
+        assert asm.count("buffer_store_dwordx4") >= 3, k  # w, alpha, momentum rows
+        waits = [int(v) for v in re.findall(r"s_waitcnt vmcnt\((\d+)\)", asm)]
+        assert any(w >= 3 for w in waits), f"{k}: no counted vmcnt wait"
