@@ -368,6 +368,48 @@ def primal_dual_round(N: int, P: int, world: int, rank: int, device, steps: int,
     return out
 
 
+def dgd_rounds(device, N: int = 1024, P: int = 1 << 20, reps: int = 10):
+    """Secondary (BASELINE config 3: synthetic least-squares / logistic, 1024
+    agents x 2^20, ring + random-regular W, mixing-bound): one decentralised
+    gradient-descent round (DIST/simulators.py:147-162: consensus, then one
+    local momentum-SGD step, DIST/clients.py:43-49) through the product
+    classes -- SeparableDGD on the agent-major bank (ring: the fused
+    dol_dgd_ring_f32) and SeparableDGDPM on the parameter-major bank (random
+    4-regular: dol_dgd_csr_pm_f32) -- each one HBM pass, bit-exact against the
+    oracle (tests/test_dgd_gpu.py, tests/test_pmajor_gpu.py).  Algorithmic
+    bytes N*P*4 * (x + y + target [+ momentum in + out])."""
+    from dolhip import graph as G
+    from dolhip.synthetic import SeparableDGD, SeparableDGDPM
+    torch.manual_seed(2028)
+    ring_plan = G.MixingPlan(G.communication_csr("circle", "stochastic", N)[0], device)
+    rr_plan = G.MixingPlan(G.random_regular_csr(N, 4, seed=2028), device)
+    out = {}
+    for name, cls, plan in (("ring", SeparableDGD, ring_plan), ("rr4_pm", SeparableDGDPM, rr_plan)):
+        for objective, mom in (("least_squares", 0.9), ("logistic", 0.0)):
+            prob = cls(plan, P, objective=objective, lr=0.01, momentum=mom, local_steps=1, seed=7)
+            for _ in range(2):
+                prob.round()
+            torch.cuda.synchronize(device)
+            _warm(prob.round, seconds=0.1)
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(reps):
+                prob.round()
+            e.record()
+            torch.cuda.synchronize(device)
+            ms = s.elapsed_time(e) / reps
+            alg = N * P * 4 * (3 + (2 if mom else 0))
+            out[f"{name}_{objective}"] = {"ms_per_round": ms, "rounds_per_s": 1e3 / ms, "momentum": mom,
+                                          "GBps": alg / (ms / 1e3) / 1e9,
+                                          "frac": alg / (ms / 1e3) / 1e9 / HBM_PEAK_GBPS,
+                                          "class": cls.__name__}
+            del prob
+            torch.cuda.empty_cache()
+    return {"agents": N, "params": P, "local_steps": 1, "rounds": out,
+            "what": "config 3 DGD round: mix + one local SGD step in one pass (ring: agent-major bank; random "
+                    "4-regular: parameter-major bank), least squares with momentum 0.9 and logistic without"}
+
+
 def _warm(fn, seconds: float = 0.25) -> None:
     """Run fn() back to back for ~seconds before a short leg is timed: after an
     idle gap the GPU's clocks take tens of ms to ramp, and a 10-rep leg of
@@ -798,6 +840,10 @@ def main():
                 secondary_errors.append({"leg": "config5_round", "error": cfg5["error"]})
                 _log(f"ERROR: config-5 round over ranks failed: {cfg5['error']}")
     _log("config 5 round done")
+    dgd = None
+    if world == 1 and not args.no_primal_dual:
+        dgd = dgd_rounds(device)
+    _log("config 3 rounds done")
 
     traffic = None
     traffic_src = None
@@ -872,6 +918,7 @@ def main():
             "dense_er_mix": dense,
             "er_exact_mix": exact,
             "config5_round": cfg5,
+            "config3_dgd": dgd,
             "secondary_errors": secondary_errors,
             "tuned_launches": ops.tuned_choices(),
         }
