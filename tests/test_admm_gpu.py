@@ -117,7 +117,7 @@ def test_admm_ls_round_argument_errors(gpu):
 
 @pytest.mark.parametrize("P,extra", [(4096, 0), (1031, 0), (1031, 1), (3, 0), (5000, 3), (70001, 0)])
 @pytest.mark.parametrize("mom,steps", [(0.5, 3), (0.0, 1), (0.9, 0)])
-@pytest.mark.parametrize("m", [5, 1])
+@pytest.mark.parametrize("m", [5, 1, 6, 9])
 def test_admm_ls_round_mean_vs_oracle(P, extra, mom, steps, m, gpu):
     """dol_admm_ls_round_mean_f32 (client round + ordered mean in one pass):
     rows bit-identical to oracle.admm_ls_round, theta_out to oracle.ordered_mean
@@ -138,8 +138,9 @@ def test_admm_ls_round_mean_vs_oracle(P, extra, mom, steps, m, gpu):
     B = rng.standard_normal((N, P)).astype(np.float32)
     th = rng.standard_normal(P).astype(np.float32)
     T[1, :3] = [np.inf, -0.0, 1e-40][:min(3, P)]
-    order = np.array([7, 2, 0, 8, 5], np.int32)[:m]
-    first = np.array([1, 0, 1, 0, 0], np.int32)[:m]
+    # groups of three agents in flight: m = 6 / 9 end on a full group, 5 / 1 on a partial one
+    order = np.array([7, 2, 0, 8, 5, 3, 6, 4, 1], np.int32)[:m]
+    first = np.array([1, 0, 1, 0, 0, 1, 1, 0, 0], np.int32)[:m]
     for scale in (None, 1.0):
         w, a, b, t = mat(np.zeros((N, P), np.float32)), mat(A), mat(B), mat(T)
         tot = torch.full((2,), float("nan"), dtype=torch.float64, device=gpu)
