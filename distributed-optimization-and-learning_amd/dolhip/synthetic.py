@@ -226,7 +226,7 @@ class SeparableADMM:
         equal to ~1e-15 relative)."""
         dev = self.device
         ml = len(local)
-        s = torch.zeros(2, dtype=torch.float64, device=dev)
+        s = torch.zeros(2, dtype=torch.float64, device=dev) if self.metrics else None
         if ml:
             rows = torch.as_tensor(local, dtype=torch.int32, device=dev)
             first = None
@@ -235,7 +235,7 @@ class SeparableADMM:
             self._round_mean(self.w, self.alpha, self.target, self.theta, agents=rows, first=first, buf=self.mom,
                              rho=self.rho, lr=self.lr, momentum=self.mu, local_steps=self.local_steps,
                              out=self._theta_next, scale=float(self.m) if self.world == 1 else 1.0,
-                             resid_total=s if self.metrics else None, P=self.P)
+                             resid_total=s, P=self.P)
             if self.mom is not None and self.local_steps > 0:
                 self.mom_started[local] = True
         else:  # a rank without sampled rows ('fast' mean): contributes zeros

@@ -205,3 +205,35 @@ def test_admm_ls_round_mean_argument_errors(gpu):
         ops.admm_ls_round_mean(w, w.clone(), w.clone(), th, resid_total=torch.zeros(1, dtype=torch.float64, device=gpu))
     with pytest.raises(ValueError, match="at least one"):
         ops.admm_ls_round_mean(w, w.clone(), w.clone(), th, agents=torch.zeros(0, dtype=torch.int32, device=gpu))
+
+
+def test_admm_ls_round_mean_defaults_and_no_metrics(gpu):
+    """agents=None means rows 0..n-1 in order (same bits as passing arange), and
+    a round without residual outputs (metrics=False: the RESID-free kernel)
+    leaves the same rows and theta as one with them."""
+    rng = np.random.default_rng(11)
+    N, P = 7, 4099
+    T = torch.as_tensor(rng.standard_normal((N, P)).astype(np.float32), device=gpu)
+    A0 = torch.as_tensor((0.1 * rng.standard_normal((N, P))).astype(np.float32), device=gpu)
+    th = torch.as_tensor(rng.standard_normal(P).astype(np.float32), device=gpu)
+    outs = []
+    for agents, tot in ((None, None), (torch.arange(N, dtype=torch.int32, device=gpu),
+                                       torch.zeros(2, dtype=torch.float64, device=gpu))):
+        w, a, b = torch.zeros(N, P, device=gpu), A0.clone(), torch.zeros(N, P, device=gpu)
+        o = ops.admm_ls_round_mean(w, a, T, th, agents=agents, buf=b, momentum=0.5, local_steps=3, resid_total=tot,
+                                   P=P)
+        torch.cuda.synchronize()
+        outs.append([x.cpu().numpy() for x in (w, a, b, o)])
+    for x, y in zip(*outs):
+        assert bits_equal(x, y)
+    kw = dict(rho=0.1, lr=0.1, momentum=0.5, local_steps=2, frac=0.5, seed=3, device=gpu)
+    s1 = SeparableADMM(21, 3001, metrics=False, **kw)
+    s2 = SeparableADMM(21, 3001, metrics=True, **kw)
+    assert s1.fused and s2.fused
+    for _ in range(3):
+        s1.round()
+        s2.round()
+    torch.cuda.synchronize()
+    assert bits_equal(s1.theta.cpu().numpy(), s2.theta.cpu().numpy())
+    assert bits_equal(s1.alpha.cpu().numpy(), s2.alpha.cpu().numpy())
+    assert s1.history == [] and len(s2.history) == 3
