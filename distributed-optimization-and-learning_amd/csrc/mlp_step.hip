@@ -462,7 +462,8 @@ __device__ __forceinline__ void mlp_fwd_body(MlpArgs a, float* __restrict__ ws) 
       k = k < d ? k : 0;  // clamped in-bounds; zeroed after landing
       const float* src = (r < h) ? top + oW1 + int64_t(r) * d + k
                                  : xa + int64_t(min(r - h, B - 1)) * a.ldxb + k;
-      __builtin_amdgcn_global_load_lds(DOL_GPTR(src), DOL_LPTR(st + ins * 256), 16, 0, 0);
+      // nontemporal (r05: fused step 0.489-0.491 vs 0.496-0.499 ms, profiles/r05zzf_mlp_load_policy_ab.jsonl)
+      __builtin_amdgcn_global_load_lds(DOL_GPTR(src), DOL_LPTR(st + ins * 256), 16, 0, 2);
     }
   };
   // PH 3: W1[32 wave + li][32 kc + 16 hh + 4 j + q] = wres[kc][j][q] (the last KL chunks: park)
