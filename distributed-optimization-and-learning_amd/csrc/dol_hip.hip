@@ -819,11 +819,15 @@ __global__ __launch_bounds__(kThreads) void prox_sgd_kernel(
   if (c >= ncols_v) return;
   V* wp = reinterpret_cast<V*>(W + agent * ldw + c_off) + c;
   V* gp = reinterpret_cast<V*>(G + agent * ldg + c_off) + c;
-  V w = *wp, g = *gp;
+  // every per-agent row is read and written once: nontemporal both ways (r05:
+  // 100 x 1,663,370 0.83 vs 0.90 ms, 1024 x 2^20 4.67 vs 4.96 ms,
+  // profiles/r05zzr_prox_sgd_nt_ab.jsonl); theta is shared by all agents: cached
+  constexpr bool DOL_PROX_NT = true;
+  V w = ldv<V, DOL_PROX_NT>(wp), g = ldv<V, DOL_PROX_NT>(gp);
   V bf{}, th{}, al{};
-  if constexpr (MODE == 2) bf = *(reinterpret_cast<V*>(B + agent * ldb + c_off) + c);
+  if constexpr (MODE == 2) bf = ldv<V, DOL_PROX_NT>(reinterpret_cast<V*>(B + agent * ldb + c_off) + c);
   if constexpr (THETA) th = *(reinterpret_cast<const V*>(theta + c_off) + c);
-  if constexpr (ALPHA) al = *(reinterpret_cast<const V*>(A + agent * lda + c_off) + c);
+  if constexpr (ALPHA) al = ldv<V, DOL_PROX_NT>(reinterpret_cast<const V*>(A + agent * lda + c_off) + c);
   if constexpr (Vec<V>::W == 1) {
     prox_sgd_lane<THETA, ALPHA, MODE, WRITE_G, DUAL>(w, bf, g, th, al, rho, neg_lr, mom);
   } else {
@@ -837,10 +841,10 @@ __global__ __launch_bounds__(kThreads) void prox_sgd_kernel(
       al[j] = aj;
     }
   }
-  *wp = w;
-  if constexpr (WRITE_G) *gp = g;
-  if constexpr (MODE != 0) *(reinterpret_cast<V*>(B + agent * ldb + c_off) + c) = bf;
-  if constexpr (DUAL) *(reinterpret_cast<V*>(A + agent * lda + c_off) + c) = al;
+  stv<V, DOL_PROX_NT>(wp, w);
+  if constexpr (WRITE_G) stv<V, DOL_PROX_NT>(gp, g);
+  if constexpr (MODE != 0) stv<V, DOL_PROX_NT>(reinterpret_cast<V*>(B + agent * ldb + c_off) + c, bf);
+  if constexpr (DUAL) stv<V, DOL_PROX_NT>(reinterpret_cast<V*>(A + agent * lda + c_off) + c, al);
 }
 
 // Gradient term alone: g += rho*(w - theta) (+ alpha), w untouched.
@@ -908,17 +912,20 @@ __global__ __launch_bounds__(kThreads) void admm_dual_kernel(
     for (int it = 0; it < kDualIters; ++it) {
       const int64_t c = (chunk * kDualIters + it) * kThreads + threadIdx.x;
       if (c < n4) {
+        // rows read / written once: nontemporal (r05: 100 x 1,663,370 0.378 vs
+        // 0.395 ms, 1024 x 2^20 2.16 vs 2.37 ms, profiles/r05zzs_admm_dual_nt_ab.jsonl)
+        constexpr bool DOL_DUAL_NT = true;
         f4* ap = reinterpret_cast<f4*>(arow) + c;
-        const f4 w = reinterpret_cast<const f4*>(wrow)[c];
+        const f4 w = ldv<f4, DOL_DUAL_NT>(reinterpret_cast<const f4*>(wrow) + c);
         const f4 th = reinterpret_cast<const f4*>(theta)[c];
-        f4 a = *ap;
+        f4 a = ldv<f4, DOL_DUAL_NT>(ap);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           float aj = a[j];
           dual_lane(aj, w[j], th[j], rho, r);
           a[j] = aj;
         }
-        *ap = a;
+        stv<f4, DOL_DUAL_NT>(ap, a);
       }
     }
     const int64_t tail = P - 4 * n4;
