@@ -8,6 +8,11 @@ kernel).  Inputs are synthetic fp32 (randn), resident in HBM before timing.
   python bench.py [--gpus N --steps K --warmup W]
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
+Without a launcher, `--gpus N > 1` starts the N ranks itself (child
+processes, before any GPU call) and relays rank 0's line; a run whose joined
+world differs from --gpus exits non-zero.  The line's `parallel` field lists
+the world size, backend and device each rank saw.
+
 Strong scaling: the 8192 agents are split into contiguous blocks, one per
 rank; each round exchanges the two boundary rows with the neighbouring ranks
 (RCCL send/recv) while the interior rows are mixed.
@@ -64,7 +69,136 @@ def parse():
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic_ring_8192x1M.json"))
     ap.add_argument("--no-primal-dual", action="store_true", help="skip the secondary measurements (primal/dual round, FedLCon eps=5, dense ER mix)")
     ap.add_argument("--pd-steps", type=int, default=10)
+    ap.add_argument("--launch-check", action="store_true",
+                    help="only bring the ranks up: every rank joins the process group and rank 0 prints the "
+                         "world each rank saw (the launcher's own test; no kernels, no GPU needed under gloo)")
     return ap.parse_args()
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv) -> int:
+    """`python bench.py --gpus N` without a launcher: start
+    N copies of this script as child processes, one rank each (RANK /
+    LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT in their
+    environment, exactly what torch.distributed.run sets), relay rank 0's JSON
+    line, and return non-zero if any rank fails or the line reports a world
+    other than N.  This process never touches the GPU (no HIP call before or
+    after the children start; they are children, not an exec).  A rank that
+    dies takes the others down at once instead of leaving them in a
+    collective until its timeout."""
+    import signal
+    import subprocess
+    import threading
+    port = int(os.environ.get("MASTER_PORT") or _free_port())
+    procs = []
+    lines: list = []
+
+    def relay(stream):  # rank 0's stdout: the JSON line (anything else goes to stderr)
+        for raw in stream:
+            s = raw.decode(errors="replace").rstrip("\n")
+            if s.startswith("{"):
+                lines.append(s)
+            else:
+                print(s, file=sys.stderr, flush=True)
+
+    def stop_all():
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, signal.SIGTERM)
+                except ProcessLookupError:
+                    pass
+        t_end = time.time() + 20
+        for p in procs:
+            try:
+                p.wait(timeout=max(0.1, t_end - time.time()))
+            except subprocess.TimeoutExpired:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+                p.wait()
+
+    reader = None
+    try:
+        for r in range(n):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                       GROUP_RANK="0", ROLE_RANK=str(r), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                       DOL_BENCH_LAUNCHER="bench.py --gpus (child processes)")
+            procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env,
+                                          stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno(),
+                                          start_new_session=True))
+        reader = threading.Thread(target=relay, args=(procs[0].stdout,), daemon=True)
+        reader.start()
+        failed = None
+        while failed is None and any(p.poll() is None for p in procs):
+            for r, p in enumerate(procs):
+                if p.poll() not in (None, 0):
+                    failed = (r, p.returncode)
+                    break
+            time.sleep(0.2)
+        if failed is None:
+            failed = next(((r, p.returncode) for r, p in enumerate(procs) if p.returncode != 0), None)
+        if failed is not None:
+            _log(f"ERROR: rank {failed[0]} exited with {failed[1]}; stopping the other ranks")
+            stop_all()
+            return failed[1] if failed[1] > 0 else 1
+    except BaseException:
+        stop_all()
+        raise
+    reader.join(timeout=10)
+    if len(lines) != 1:
+        _log(f"ERROR: rank 0 printed {len(lines)} JSON lines, expected one")
+        return 1
+    got = json.loads(lines[0]).get("n_gpus")
+    if got != n:
+        _log(f"ERROR: the line reports n_gpus={got}, launched {n} ranks")
+        return 1
+    print(lines[0], flush=True)
+    return 0
+
+
+def rank_infos(world: int, rank: int, local: int, backend: str, device) -> list:
+    """What every rank saw (world size, rank, backend, device), gathered to all
+    ranks: the line's `parallel` field, so a run that came up with fewer ranks
+    than asked cannot pass for an N-GPU number."""
+    me = {"rank": rank, "local_rank": local, "world_size": world,
+          "backend": dist.get_backend() if world > 1 else "none", "device": str(device), "pid": os.getpid(),
+          "launcher": os.environ.get("DOL_BENCH_LAUNCHER", "torch.distributed.run" if world > 1 else "none")}
+    if world == 1:
+        return [me]
+    out = [None] * world
+    dist.all_gather_object(out, me)
+    return out
+
+
+def launch_check(args, world: int, rank: int, local: int, backend: str) -> int:
+    """--launch-check: join the group, gather what each rank saw, rank 0 prints
+    one JSON line in the bench line's shape (n_gpus, parallel); no kernels."""
+    from dolhip import parallel
+    if world > 1:
+        dev = None
+        if backend == "nccl":
+            dev = torch.device("cuda", int(os.environ.get("DOL_DEVICE_MAP", local)))
+            torch.cuda.set_device(dev)
+        parallel.init_process_group(backend, device=dev)
+    infos = rank_infos(world, rank, local, backend, "cpu" if backend == "gloo" else f"cuda:{local}")
+    if os.environ.get("DOL_BENCH_FAIL_RANK") == str(rank):  # tests: a rank that dies after joining
+        os._exit(3)
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world, "steps": 0,
+                          "parallel": {"world_size": world, "backend": infos[0]["backend"], "ranks": infos}}),
+              flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
 
 
 def ring_weights(n: int):
@@ -356,9 +490,35 @@ def primal_dual_round(N: int, P: int, world: int, rank: int, device, steps: int,
                  "bytes_moved_per_rank": prob.n * P * 4 * (world - 1) // world,
                  "what": "global_mean_exact: all_to_all of the sampled rows to column blocks + ordered sum + all_gather"}
     hist = prob.history
+    columns = None
+    if world > 1:
+        # the parameter-sharded problem: every rank runs all
+        # sampled agents on its column block, theta exact, no collective per round
+        del prob
+        torch.cuda.empty_cache()
+        colp = SeparableADMM(N, P, rho=0.1, lr=0.1, momentum=0.5, local_steps=local_steps, frac=1.0, seed=2028,
+                             device=device, shard="columns")
+        colp.round()
+        torch.cuda.synchronize(device)
+        dist.barrier()
+        t1 = time.perf_counter()
+        for _ in range(steps):
+            colp.round()
+        torch.cuda.synchronize(device)
+        dist.barrier()
+        tc = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=device)
+        dist.all_reduce(tc, op=dist.ReduceOp.MAX)
+        cms = float(tc.item()) / steps * 1e3
+        colp.history  # (collective: the metric partials summed across ranks)
+        columns = {"rounds_per_s": 1e3 / cms, "ms_per_round": cms, "columns_per_rank": colp.Pl,
+                   "GBps_per_rank": (6 * N * colp.Pl + 2 * colp.Pl) * 4 / (cms / 1e3) / 1e9,
+                   "what": "SeparableADMM(shard='columns'): dol_admm_ls_round_mean_f32 over all sampled agents on "
+                           "this rank's parameter columns, theta bit-exact (DEC/servers.py:42-48's order), no "
+                           "collective on the round path"}
+        prob = colp
     out = {"rounds_per_s": steps / el, "ms_per_round": el / steps * 1e3, "agents": N, "params": P,
            "local_steps": local_steps, "kernels": kern, "fused_round_mean": fused, "two_kernel_round": two_kernel,
-           "exact_mean": exact,
+           "exact_mean": exact, "column_sharded_exact": columns,
            "primal_resid_sq_last": hist[-1]["primal_resid_sq"], "dual_sq_last": hist[-1]["dual_sq"],
            "what": "FedADMM least-squares round over all agents: fused client round (w = theta, %d momentum-SGD "
                    "steps with the ADMM term, dual ascent) with this rank's ordered sum of the new rows in the "
@@ -452,8 +612,8 @@ def fedlcon_eps_round(device, ring, N: int, P: int, eps: int = 5, reps: int = 10
     plan = G.MixingPlan(G.communication_csr("circle", "stochastic", N)[0], device)
     assert plan.kind == "ring"
     bank = AgentBank(N, P, device, ld=ring.x.stride(0))
-    bank.adopt("x", ring.x)
-    bank.adopt("y", ring.y)
+    bank.adopt("x", ring.x, replaceable=True)
+    bank.adopt("y", ring.y, replaceable=True)  # dead contents: the destination check may swap them
     # first uses: the destination check of each (source, destination) pair
     # (AgentBank.mix; a slow destination is replaced) and the eps
     # kernel's tuning for each buffer pair -- until a call adds no check
@@ -718,17 +878,23 @@ def config5_round(device, N: int = 1024, reps: int = 10):
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no launcher around us: start the N ranks ourselves (before any GPU call)
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if rank == 0:
-            print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+        # a line timed on fewer (or more) ranks than asked would pass for the wrong N
+        print(f"error: --gpus {args.gpus} but WORLD_SIZE={world} ranks joined", file=sys.stderr, flush=True)
+        sys.exit(2)
     # DOL_DEVICE_MAP=0 puts every rank on cuda:0 and DOL_DIST_BACKEND=gloo stages
     # halos through host memory: a rehearsal of the N>1 path on a 1-GPU box
+    backend = os.environ.get("DOL_DIST_BACKEND", "nccl")
+    if args.launch_check:
+        sys.exit(launch_check(args, world, rank, local, backend))
     device = torch.device("cuda", int(os.environ.get("DOL_DEVICE_MAP", local)))
     torch.cuda.set_device(device)
-    backend = os.environ.get("DOL_DIST_BACKEND", "nccl")
     import dolhip
     from dolhip import parallel
     from dolhip.parallel import ShardedRing
@@ -736,6 +902,7 @@ def main():
         # bounded timeout on every collective + RCCL async error handling: a
         # stuck rank fails the run instead of hanging it
         parallel.init_process_group(backend, device=device if backend == "nccl" else None)
+    infos = rank_infos(world, rank, local, backend, device)
 
     dolhip.lib()
     N, P = args.agents, args.params
@@ -857,6 +1024,8 @@ def main():
             traffic = None
 
     from dolhip import ops
+    from dolhip.bank import retired_va
+    bank_va = retired_va()
     out = None
     if rank == 0:
         cpu = None
@@ -894,6 +1063,9 @@ def main():
                 "parallelism": f"agent-shard x{world}" + ((" + RCCL halo send/recv" if backend == "nccl" else
                                                            f" + {backend} halo send/recv (rehearsal)") if world > 1 else ""),
             },
+            "parallel": {"world_size": world, "backend": infos[0]["backend"],
+                         "distinct_devices": len({(i["device"]) for i in infos}),
+                         "launcher": infos[0]["launcher"], "ranks": infos},
             "roofline": {
                 "bound": "hbm",
                 "kernel": ("ring_mix_kernel" if os.environ.get("DOL_RING_DMA", "1") == "0" else
@@ -921,6 +1093,7 @@ def main():
             "config3_dgd": dgd,
             "secondary_errors": secondary_errors,
             "tuned_launches": ops.tuned_choices(),
+            "bank_retired_va": bank_va,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

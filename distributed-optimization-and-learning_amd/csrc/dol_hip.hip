@@ -1657,6 +1657,26 @@ struct BankBlock {
 };
 static std::mutex g_bank_mu;  // dol_bank_alloc's live blocks: VA -> physical handle + mapped size
 static std::unordered_map<void*, BankBlock> g_bank_handles;
+// Virtual address space retired by dol_bank_free (see there) -- counted, and
+// capped: past the cap dol_bank_alloc refuses new blocks instead of reserving
+// address space without bound.  Guarded by g_bank_mu.
+static int64_t g_bank_retired = 0;
+static int64_t g_bank_retired_blocks = 0;
+
+int64_t dol_bank_retired_cap_bytes(void) {
+  const int64_t gib = env_int("DOL_BANK_RETIRED_VA_CAP_GIB", 4096);  // 4 TiB: 128 retired 32 GiB matrices
+  return gib > 0 ? gib << 30 : 0;
+}
+
+int64_t dol_bank_retired_bytes(void) {
+  std::lock_guard<std::mutex> lk(g_bank_mu);
+  return g_bank_retired;
+}
+
+int64_t dol_bank_retired_blocks(void) {
+  std::lock_guard<std::mutex> lk(g_bank_mu);
+  return g_bank_retired_blocks;
+}
 
 // A bank buffer as ONE physical allocation (hipMemCreate) mapped into a
 // reserved VA range, instead of whatever hipMalloc's suballocator returns
@@ -1676,6 +1696,17 @@ int dol_bank_alloc(int64_t bytes, void** ptr, int64_t* mapped_bytes) {
   hipError_t e = hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended);
   if (e != hipSuccess || gran == 0) return fail(-static_cast<int>(e ? e : hipErrorInvalidValue), "dol_bank_alloc: granularity: %s", hipGetErrorString(e));
   const size_t size = (static_cast<size_t>(bytes) + gran - 1) / gran * gran;
+  if (!env_int("DOL_BANK_FREE_VA", 0)) {  // this block's range will be retired when freed: stay under the cap
+    std::lock_guard<std::mutex> lk(g_bank_mu);
+    int64_t live = 0;
+    for (const auto& kv : g_bank_handles) live += static_cast<int64_t>(kv.second.size);
+    const int64_t cap = dol_bank_retired_cap_bytes();
+    if (g_bank_retired + live + static_cast<int64_t>(size) > cap)
+      return fail(DOL_ECAP, "dol_bank_alloc: %zu bytes would take the retired + live mapped address space "
+                  "(%lld + %lld bytes) past its cap of %lld bytes (DOL_BANK_RETIRED_VA_CAP_GIB); use torch's "
+                  "allocator (DOL_BANK_ALLOC=torch)", size, static_cast<long long>(g_bank_retired),
+                  static_cast<long long>(live), static_cast<long long>(cap));
+  }
   hipMemGenericAllocationHandle_t h{};
   if ((e = hipMemCreate(&h, size, &prop, 0)) != hipSuccess)
     return fail(-static_cast<int>(e), "dol_bank_alloc: hipMemCreate(%zu): %s", size, hipGetErrorString(e));
@@ -1738,7 +1769,11 @@ int dol_bank_free(void* ptr, int64_t mapped_bytes) {
     // translation to a released range is also the r04k illegal-address fault.
     // Retiring costs address space only (the physical memory is released).
     // DOL_BANK_FREE_VA=1 restores the freeing order (diagnostics only).
+    // Counted in g_bank_retired (dol_bank_retired_bytes) against the cap that
+    // dol_bank_alloc enforces.
     blk.stage = 2;
+    g_bank_retired += static_cast<int64_t>(blk.size);
+    g_bank_retired_blocks += 1;
   }
   if (blk.stage == 1) {
     if ((e = hipMemAddressFree(ptr, blk.size)) != hipSuccess)

@@ -84,13 +84,17 @@ SIGNATURES = {
     "dol_dense_to_csr_f32": [_ptr, _i64, _i32, _i32, _ptr, _ptr, _ptr, _i64, _ptr],
     "dol_bank_alloc": [_i64, _ptr, _ptr],  # (bytes, void** out, int64_t* out): addresses of host words
     "dol_bank_free": [_ptr, _i64],
+    "dol_bank_retired_bytes": [],
+    "dol_bank_retired_blocks": [],
+    "dol_bank_retired_cap_bytes": [],
 }
 _RESTYPES = {"dol_last_error": ctypes.c_char_p, "dol_admm_dual_workspace_bytes": ctypes.c_int64,
              "dol_admm_ls_round_workspace_bytes": ctypes.c_int64,
              "dol_admm_ls_round_mean_workspace_bytes": ctypes.c_int64,
              "dol_mlp_step_lds_bytes": ctypes.c_int64, "dol_mlp_step_workspace_bytes": ctypes.c_int64,
              "dol_mix_dense_split3_workspace_bytes": ctypes.c_int64, "dol_csr_slab_hdr_len": ctypes.c_int64,
-             "dol_csr_slab_ent_len": ctypes.c_int64}
+             "dol_csr_slab_ent_len": ctypes.c_int64, "dol_bank_retired_bytes": ctypes.c_int64,
+             "dol_bank_retired_blocks": ctypes.c_int64, "dol_bank_retired_cap_bytes": ctypes.c_int64}
 
 _lib = None
 

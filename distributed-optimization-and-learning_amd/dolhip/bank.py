@@ -131,6 +131,16 @@ def release_leaked() -> int:
 
 
 MAPPED_MIN_BYTES = 1 << 30
+_CAP_WARNED = []
+
+
+def retired_va() -> dict:
+    """Address space retired by dol_bank_free (freed mapped blocks keep their
+    virtual range reserved) and its cap (dol_bank_alloc refuses
+    new mapped blocks past it)."""
+    L = _native.lib()
+    return {"bytes": int(L.dol_bank_retired_bytes()), "blocks": int(L.dol_bank_retired_blocks()),
+            "cap_bytes": int(L.dol_bank_retired_cap_bytes())}
 
 
 def device_matrix(rows: int, cols: int, device, zero: bool = False, mapped: Optional[bool] = None) -> torch.Tensor:
@@ -148,14 +158,29 @@ def device_matrix(rows: int, cols: int, device, zero: bool = False, mapped: Opti
     wrong, profiles/r05c_vmm_remap_probe.jsonl).  dol_bank_free now retires
     the range instead of freeing it, and twelve map/free cycles are bit-exact
     (tests/test_bank_alloc_gpu.py::test_mapped_blocks_survive_map_free_remap_cycles).
-    mapped=True / False decides for this matrix regardless of the environment."""
+    mapped=True / False decides for this matrix regardless of the environment.
+    Retired address space is counted and capped (retired_va()): past the cap
+    a default (mapped=None) matrix falls back to torch's allocator with a
+    warning; mapped=True raises."""
     device = torch.device(device)
     want = os.environ.get("DOL_BANK_ALLOC", "vmm") == "vmm" if mapped is None else bool(mapped)
     if want and device.type == "cuda" and rows * cols * 4 >= MAPPED_MIN_BYTES:
-        t = torch.as_tensor(_MappedBlock(rows, cols, device), device=device)
-        if zero:
-            t.zero_()
-        return t
+        try:
+            blk = _MappedBlock(rows, cols, device)
+        except _native.DolNativeError as e:
+            if mapped is not None or "DOL_BANK_RETIRED_VA_CAP_GIB" not in str(e):
+                raise
+            if not _CAP_WARNED:
+                import warnings
+                warnings.warn(f"dolhip: {e}; bank matrices now come from torch's allocator", ResourceWarning,
+                              stacklevel=2)
+                _CAP_WARNED.append(True)
+            blk = None
+        if blk is not None:
+            t = torch.as_tensor(blk, device=device)
+            if zero:
+                t.zero_()
+            return t
     alloc = torch.zeros if zero else torch.empty
     return alloc(rows, cols, dtype=torch.float32, device=device)
 
@@ -165,14 +190,23 @@ def device_matrix(rows: int, cols: int, device, zero: bool = False, mapped: Opti
 # slower than on others (13.1-13.5 vs 11.0-11.4 ms at 8192 x 2^20, while the
 # ring round is 10.6-10.9 ms on every pair; which pairs is random per
 # allocation, any allocator).  Before a bank's fused pass first writes a
-# buffer from a given source, the pass and one ring round are timed on that
-# (source, destination) pair; when the pass is slower than PAIR_RATIO x the
-# round, the destination -- whose contents the pass is about to overwrite --
-# is replaced by a fresh allocation (up to PAIR_TRIES times, keeping the
-# fastest).  DOL_BANK_PAIR_PROBE=0 turns it off.
+# buffer from a given source, a PAIR_PROBE_STEPS-round pass and one ring round
+# are timed on that (source, destination) pair; when the pass is slower than
+# PAIR_RATIO x the round, the destination -- whose contents the pass is about
+# to overwrite -- is replaced by a fresh allocation (up to PAIR_TRIES times,
+# keeping the fastest).  The probe's step count is fixed at the one PAIR_RATIO
+# was calibrated on (eps = 5, 8192 x 2^20): the slowness belongs to the pair of
+# allocations, not to the step count, and a longer pass carries more
+# arithmetic per byte.  At most ONE candidate besides the
+# current best is held at a time (the loser is dropped before the next
+# allocation); a candidate at an address already probed (torch's caching
+# allocator hands a dropped block straight back) ends the search; buffers the
+# caller adopted are not replaced unless adopted with replaceable=True.
+# DOL_BANK_PAIR_PROBE=0 turns it off.
 PAIR_PROBE_MIN_BYTES = 4 << 30
 PAIR_RATIO = 1.12
 PAIR_TRIES = 3
+PAIR_PROBE_STEPS = 5
 
 
 def _pair_probe_ms(x: torch.Tensor, y: torch.Tensor, plan, steps: int, P: int, reps: int = 2) -> Tuple[float, float]:
@@ -194,6 +228,7 @@ class AgentBank:
         self._pair_checked: set = set()
         self.pair_probes: List[dict] = []
         self._pair_timer = _pair_probe_ms  # tests inject a timer
+        self._pinned: set = set()  # names of adopted buffers the destination check must not replace
         if isinstance(layout_or_P, int):
             self.layout: Layout = [("w", (int(layout_or_P),))]
         else:
@@ -224,14 +259,20 @@ class AgentBank:
             self._buf[name] = t
         return t
 
-    def adopt(self, name: str, t: torch.Tensor) -> None:
+    def adopt(self, name: str, t: torch.Tensor, replaceable: bool = False) -> None:
         """Use an existing [N, ld] fp32 device matrix as buffer `name` (e.g. a
-        bank over state that was allocated elsewhere)."""
+        bank over state that was allocated elsewhere).  replaceable: the fused
+        ring pass's destination check may swap it for a fresh allocation (its
+        contents are dead when replaced); otherwise it stays the caller's."""
         if (t.device != self.device or t.dtype != torch.float32 or tuple(t.shape) != (self.n, self.ld)
                 or t.stride(1) != 1 or (self.n > 1 and t.stride(0) != self.ld)):
             raise ValueError(f"adopt({name!r}): expected a float32 [{self.n}, {self.ld}] row-major matrix on "
                              f"{self.device}")
         self._buf[name] = t
+        if replaceable:
+            self._pinned.discard(name)
+        else:
+            self._pinned.add(name)
         if name == "x":
             self.rebind_all()
 
@@ -292,6 +333,13 @@ class AgentBank:
     # ------------------------------------------------------------------ mixing
     def swap(self, a: str = "x", b: str = "y") -> None:
         self._buf[a], self._buf[b] = self._buf[b], self._buf[a]
+        pa, pb = a in self._pinned, b in self._pinned  # pinning follows the tensor
+        self._pinned.discard(a)
+        self._pinned.discard(b)
+        if pa:
+            self._pinned.add(b)
+        if pb:
+            self._pinned.add(a)
         if a == "x" or b == "x":
             self.rebind_all()
 
@@ -309,9 +357,15 @@ class AgentBank:
             else:
                 plan.apply(self.buffer("x"), y, P=self.P)
                 done += 1
-            self._buf["x"], self._buf["y"] = y, self._buf["x"]
+            self.swap_xy_nobind()
             y = self._buf["y"]
         self.rebind_all()
+
+    def swap_xy_nobind(self) -> None:
+        self._buf["x"], self._buf["y"] = self._buf["y"], self._buf["x"]
+        px, py = "x" in self._pinned, "y" in self._pinned
+        self._pinned.difference_update(("x", "y"))
+        self._pinned.update(n for n, p in (("y", px), ("x", py)) if p)
 
     def _check_destination(self, plan, steps: int) -> torch.Tensor:
         """The buffer the next fused ring pass writes ("y"), replaced first if
@@ -328,21 +382,33 @@ class AgentBank:
         with torch.cuda.device(self.device):
             if torch.cuda.is_current_stream_capturing():  # no timing inside a graph capture
                 return y
+        replace = "y" not in self._pinned
         best = (float("inf"), y)
-        del self._buf["y"]  # held in y / best only: a losing candidate is freed when replaced
+        probed = set()
+        del self._buf["y"]  # held in y / best only: a losing candidate is dropped before the next allocation
         try:
             for attempt in range(PAIR_TRIES):
-                pass_ms, round_ms = self._pair_timer(x, y, plan, steps, self.P)
-                self.pair_probes.append({"attempt": attempt, "pass_ms": pass_ms, "round_ms": round_ms,
+                probed.add(y.data_ptr())
+                pass_ms, round_ms = self._pair_timer(x, y, plan, PAIR_PROBE_STEPS, self.P)
+                self.pair_probes.append({"attempt": attempt, "steps": PAIR_PROBE_STEPS, "pass_ms": pass_ms,
+                                         "round_ms": round_ms,
                                          "ratio": pass_ms / round_ms if round_ms > 0 else float("inf")})
                 if pass_ms < best[0]:
                     best = (pass_ms, y)
                 if pass_ms <= PAIR_RATIO * round_ms or attempt + 1 == PAIR_TRIES:
                     break
+                if not replace:
+                    self.pair_probes[-1]["kept_adopted"] = True
+                    break
+                y = None  # the loser (unless it is the best) goes before the next allocation
                 try:  # a fresh allocation for the destination; no memory for one: keep the best so far
                     y = device_matrix(self.n, self.ld, self.device)
                 except RuntimeError:  # torch's OOM and DolNativeError alike
                     self.pair_probes[-1]["realloc_failed"] = True
+                    break
+                if y.data_ptr() in probed:  # the allocator handed back a block already measured
+                    self.pair_probes[-1]["same_block"] = True
+                    y = None
                     break
         finally:
             y = best[1]

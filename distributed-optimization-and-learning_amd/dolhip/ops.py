@@ -877,7 +877,7 @@ def admm_ls_round_mean(w: torch.Tensor, alpha: torch.Tensor, target: torch.Tenso
                        buf: Optional[torch.Tensor] = None, rho: float = 0.1, lr: float = 0.1, momentum: float = 0.0,
                        local_steps: int = 1, out: Optional[torch.Tensor] = None, scale: Optional[float] = None,
                        resid_total: Optional[torch.Tensor] = None, work: Optional[torch.Tensor] = None,
-                       P: Optional[int] = None) -> torch.Tensor:
+                       P: Optional[int] = None, validate: bool = True) -> torch.Tensor:
     """admm_ls_round + the server's ordered average in ONE pass
     (dol_admm_ls_round_mean_f32): the rows come out as admm_ls_round leaves
     them and `out` = ordered_sum(w, agents, scale=scale) of the new rows, the
@@ -885,6 +885,12 @@ def admm_ls_round_mean(w: torch.Tensor, alpha: torch.Tensor, target: torch.Tenso
     DEC/servers.py:42-48); 1.0 = the raw ordered sum.  agents: DISTINCT rows in
     the sampled order (None = 0..n-1).  resid_total: float64 [2] output, the
     round's sums over the agents of ||w - theta||^2 and ||alpha||^2.
+    validate (default): check on the host that `agents` are distinct rows of w
+    (one device-to-host copy of m ids).  The kernel loads the next agents'
+    rows before it stores the current ones, so a repeated id would read a
+    stale row, and an out-of-range id would read and write out of bounds
+    (ADVICE r05).  Callers that drew the ids themselves on the host and
+    checked them (SeparableADMM.round) pass validate=False.
     Reference: DEC/servers.py:50-81 (Server.run's round) on least squares."""
     P = w.shape[1] if P is None else P
     ldw = _check_rows("w", w, P)
@@ -907,6 +913,12 @@ def admm_ls_round_mean(w: torch.Tensor, alpha: torch.Tensor, target: torch.Tenso
     if agents is not None:
         _check_order(agents, w.device, n)
         m = agents.numel()
+        if m > n:
+            raise ValueError(f"admm_ls_round_mean: {m} agents but w has {n} rows (agents must be distinct)")
+        if validate and m:
+            ids = agents.cpu()
+            if int(ids.min()) < 0 or int(ids.max()) >= n or torch.unique(ids).numel() != m:
+                raise ValueError(f"admm_ls_round_mean: agents must be distinct rows in [0, {n})")
     if m < 1:
         raise ValueError("admm_ls_round_mean needs at least one agent (the average indexes w[0])")
     if first is not None and (first.device != w.device or first.dtype != torch.int32 or not first.is_contiguous()

@@ -66,6 +66,14 @@ def init_process_group(backend: str, rank: Optional[int] = None, world_size: Opt
     dist.init_process_group(backend, **kw)
 
 
+def _backend(group=None) -> str:
+    """The group's backend.  Every backend-dependent branch of this module asks
+    here (tests/test_parallel_gloo.py::test_every_rccl_line_runs_under_gloo
+    answers "nccl" over a gloo group of CPU tensors, so the lines RCCL runs
+    execute on the CPU tier)."""
+    return dist.get_backend(group)
+
+
 def _wait_all(reqs, group=None) -> None:
     """Wait for point-to-point requests.  gloo: bounded by DEFAULT_TIMEOUT_S on
     the host (a recv whose peer never sends raises instead of blocking
@@ -73,10 +81,10 @@ def _wait_all(reqs, group=None) -> None:
     the host does not block; a timeout here would stall the host every round),
     with the hang bound by the group's timeout + RCCL's async error handling
     set up by init_process_group."""
-    bounded = dist.get_backend(group) == "gloo"
+    bounded = _backend(group) == "gloo"
     for r in reqs:
         if bounded:
-            r.wait(datetime.timedelta(seconds=DEFAULT_TIMEOUT_S))
+            r.wait(datetime.timedelta(seconds=DEFAULT_TIMEOUT_S))  # gloo-only
         else:
             r.wait()
 
@@ -137,7 +145,7 @@ class ShardedRing:
 
     def _staged(self) -> bool:
         """gloo cannot send device tensors: stage the halo rows through host memory."""
-        return self.device.type == "cuda" and dist.get_backend(self.group) == "gloo"
+        return self.device.type == "cuda" and _backend(self.group) == "gloo"
 
     def _exchange(self, x: torch.Tensor):
         """Post the halo send/recv pairs; returns the requests.
@@ -149,9 +157,9 @@ class ShardedRing:
         first, last = x[0, :P], x[self.n_local - 1, :P]
         hp, hn = self.halo_prev[:P], self.halo_next[:P]
         if self._staged():
-            first, last = first.cpu(), last.cpu()
-            self._host_halo = (torch.empty(P), torch.empty(P))
-            hp, hn = self._host_halo
+            first, last = first.cpu(), last.cpu()  # staged
+            self._host_halo = (torch.empty(P), torch.empty(P))  # staged
+            hp, hn = self._host_halo  # staged
         ops_ = [
             dist.P2POp(dist.isend, last, self.next_rank, self.group, tag=0),
             dist.P2POp(dist.irecv, hp, self.prev_rank, self.group, tag=0),
@@ -163,8 +171,8 @@ class ShardedRing:
     def _finish_exchange(self, reqs) -> None:
         _wait_all(reqs, self.group)
         if self._staged():
-            self.halo_prev[: self.P].copy_(self._host_halo[0])
-            self.halo_next[: self.P].copy_(self._host_halo[1])
+            self.halo_prev[: self.P].copy_(self._host_halo[0])  # staged
+            self.halo_next[: self.P].copy_(self._host_halo[1])  # staged
 
     def step(self, x: Optional[torch.Tensor] = None, y: Optional[torch.Tensor] = None) -> None:
         """One Jacobi round Y = W X on the local block (then swap if using own buffers)."""
@@ -294,7 +302,7 @@ class ColumnSharded:
         mine = self.x[:, :self.Pl].contiguous()
         if self.world == 1:
             return mine
-        staged = mine.device.type == "cuda" and dist.get_backend(self.group) == "gloo"
+        staged = mine.device.type == "cuda" and _backend(self.group) == "gloo"
         send = mine.cpu() if staged else mine
         if self.rank != dst:
             if self.Pl > 0:
@@ -367,13 +375,13 @@ class AgentColumnTranspose:
         self.plan = plan
 
     def _staged(self) -> bool:
-        return self.device.type == "cuda" and dist.get_backend(self.group) == "gloo"
+        return self.device.type == "cuda" and _backend(self.group) == "gloo"
 
     def _all_to_all(self, send: torch.Tensor, recv: torch.Tensor, send_splits, recv_splits) -> None:
         if self._staged():
-            hs, hr = send.cpu(), torch.empty(recv.shape, dtype=recv.dtype)
-            dist.all_to_all_single(hr, hs, recv_splits, send_splits, group=self.group)
-            recv.copy_(hr)
+            hs, hr = send.cpu(), torch.empty(recv.shape, dtype=recv.dtype)  # staged
+            dist.all_to_all_single(hr, hs, recv_splits, send_splits, group=self.group)  # staged
+            recv.copy_(hr)  # staged
         else:
             dist.all_to_all_single(recv, send, recv_splits, send_splits, group=self.group)
 
@@ -468,8 +476,8 @@ class AgentColumnTranspose:
             a, b = mine[c]
             ev = None
             if main is not None:
-                ev = torch.cuda.Event()
-                ev.record(main)
+                ev = torch.cuda.Event()  # device-only
+                ev.record(main)  # device-only
             if c + 1 < chunks:  # the next piece's step goes in before this piece's exchange
                 step_rows(*mine[c + 1])
             src = [self._chunk_bounds(s, chunks)[c] for s in range(self.world)]
@@ -478,7 +486,7 @@ class AgentColumnTranspose:
             stage_off += sum(m_src) * Pc
             with self._on(side):
                 if ev is not None:
-                    side.wait_event(ev)
+                    side.wait_event(ev)  # device-only
                 send = self._buf_rows[a * P:b * P]
                 off = 0
                 for qa, qb in self.col_bounds:  # to rank q: my piece's rows x its columns
@@ -498,7 +506,7 @@ class AgentColumnTranspose:
                         block[g0 + lo:g0 + hi].copy_(stage[off:off + (hi - lo) * Pc].view(hi - lo, Pc))
                     off += (hi - lo) * Pc
         if main is not None:
-            main.wait_stream(side)
+            main.wait_stream(side)  # device-only
         if before_mix is not None:
             before_mix()
         return self._mix_block_and_return(out)
@@ -506,9 +514,9 @@ class AgentColumnTranspose:
     def _side_stream(self):
         if self.device.type != "cuda":
             return None
-        if self._side is None:
-            self._side = torch.cuda.Stream(self.device)
-        return self._side
+        if self._side is None:  # device-only
+            self._side = torch.cuda.Stream(self.device)  # device-only
+        return self._side  # device-only
 
     @staticmethod
     def _on(stream):
@@ -518,15 +526,15 @@ class AgentColumnTranspose:
     def _post_all_to_all(self, recv: torch.Tensor, send: torch.Tensor, recv_splits, send_splits):
         """Start an all_to_all_single on the current stream's data; returns a handle."""
         if self._staged():
-            hs, hr = send.cpu(), torch.empty(recv.shape, dtype=recv.dtype)
-            return dist.all_to_all_single(hr, hs, recv_splits, send_splits, group=self.group, async_op=True), hr
+            hs, hr = send.cpu(), torch.empty(recv.shape, dtype=recv.dtype)  # staged
+            return dist.all_to_all_single(hr, hs, recv_splits, send_splits, group=self.group, async_op=True), hr  # staged
         return dist.all_to_all_single(recv, send, recv_splits, send_splits, group=self.group, async_op=True), None
 
     def _finish_all_to_all(self, handle, recv: torch.Tensor) -> None:
         work, host = handle
         if host is not None:
-            _wait_all([work], self.group)
-            recv.copy_(host)
+            _wait_all([work], self.group)  # staged
+            recv.copy_(host)  # staged
         else:
             work.wait()  # the current stream waits for the transfer (RCCL: stream-side)
 
@@ -596,10 +604,10 @@ def global_mean_finish(out: torch.Tensor, m_total: int, P: int, group=None, orde
     ordered_sum = ordered_sum if ordered_sum is not None else ops.ordered_sum
     device = out.device
     if dist.is_initialized() and dist.get_world_size(group) > 1:
-        if out.device.type == "cuda" and dist.get_backend(group) == "gloo":
-            host = out.cpu()
-            dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)
-            out.copy_(host)
+        if out.device.type == "cuda" and _backend(group) == "gloo":
+            host = out.cpu()  # staged
+            dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)  # staged
+            out.copy_(host)  # staged
         else:
             dist.all_reduce(out, op=dist.ReduceOp.SUM, group=group)
     zero = torch.empty(0, dtype=torch.int32, device=device)
@@ -693,35 +701,38 @@ def _all_to_all(recv: torch.Tensor, send: torch.Tensor, recv_splits, send_splits
     """all_to_all_single over the first sum(splits) elements (gloo: staged through host memory)."""
     ns, nr = int(sum(send_splits)), int(sum(recv_splits))
     if _gloo_staged(send, group):
-        hs, hr = send[:ns].cpu(), torch.empty(nr, dtype=recv.dtype)
-        dist.all_to_all_single(hr, hs, list(recv_splits), list(send_splits), group=group)
-        recv[:nr].copy_(hr)
+        hs, hr = send[:ns].cpu(), torch.empty(nr, dtype=recv.dtype)  # staged
+        dist.all_to_all_single(hr, hs, list(recv_splits), list(send_splits), group=group)  # staged
+        recv[:nr].copy_(hr)  # staged
     else:
         dist.all_to_all_single(recv[:nr], send[:ns], list(recv_splits), list(send_splits), group=group)
 
 
 def _all_gather(t: torch.Tensor, group) -> List[torch.Tensor]:
-    """Every rank's `t` (equal sizes), in rank order (gloo: staged through host memory)."""
+    """Every rank's `t` (equal sizes), in rank order: one all_gather_into_tensor
+    into a [world, numel] block on every backend (gloo: device tensors staged
+    through host memory)."""
     world = dist.get_world_size(group)
-    if dist.get_backend(group) == "gloo":
-        src = t.cpu() if t.device.type == "cuda" else t
-        outs = [torch.empty_like(src) for _ in range(world)]
-        dist.all_gather(outs, src, group=group)
-        return [o.to(t.device) for o in outs] if t.device.type == "cuda" else outs
-    flat = torch.empty(world * t.numel(), dtype=t.dtype, device=t.device)
-    dist.all_gather_into_tensor(flat, t, group=group)
+    staged = _gloo_staged(t, group)
+    src = t.contiguous()
+    if staged:
+        src = src.cpu()  # staged
+    flat = torch.empty(world * t.numel(), dtype=t.dtype, device=src.device)
+    dist.all_gather_into_tensor(flat, src, group=group)
+    if staged:
+        flat = flat.to(t.device)  # staged
     return list(flat.view(world, t.numel()))
 
 
 def _gloo_staged(t: torch.Tensor, group) -> bool:
     """gloo reads raw host pointers: device tensors go through host memory."""
-    return t.device.type == "cuda" and dist.get_backend(group) == "gloo"
+    return t.device.type == "cuda" and _backend(group) == "gloo"
 
 
 def _all_bounds(lo: int, hi: int, device, group=None) -> List[Tuple[int, int]]:
     world = dist.get_world_size(group)
     mine = torch.tensor([lo, hi], dtype=torch.int64)  # host: tiny, and valid for gloo and RCCL via .to()
-    if not (torch.device(device).type == "cuda" and dist.get_backend(group) == "gloo"):
+    if not (torch.device(device).type == "cuda" and _backend(group) == "gloo"):
         mine = mine.to(device)
     allb = [torch.empty_like(mine) for _ in range(world)]
     dist.all_gather(allb, mine, group=group)

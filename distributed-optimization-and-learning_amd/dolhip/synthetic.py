@@ -107,15 +107,26 @@ class SeparableADMM:
     buf = g'.  Metrics per round: sum over sampled clients of
     ||w_k - theta||^2 (primal residual, pre-round theta) and ||alpha_k||^2.
 
-    Sharded: with torch.distributed initialised, rank r owns the contiguous
-    agent block parallel.shard_bounds(N, world, r); every rank draws the same
-    order (same seed), runs its local sampled rows, and the mean is the only
-    collective.  `round_fn` / `ordered_sum` inject CPU checkers in tests.
+    Sharded (torch.distributed initialised), two ways:
+      shard="agents": rank r owns the contiguous agent block
+        parallel.shard_bounds(N, world, r); every rank draws the same order
+        (same seed), runs its local sampled rows, and the mean is the only
+        collective ("exact": parallel.global_mean_exact, "fast": all_reduce).
+      shard="columns" (VERDICT r05 item 6): rank r owns EVERY
+        agent x the parameter columns parallel.column_bounds(P, world, r).  The
+        objective is separable per coordinate, so each rank runs the fused round
+        + ordered mean (dol_admm_ls_round_mean_f32) over all sampled agents on
+        its columns, in the global sampled order: theta's block is exactly
+        DEC/servers.py:42-48's mean with NO collective on the round path.  The
+        residual metrics are per-rank partials, summed across ranks when
+        `history` is read (a collective: every rank reads it).
+    `round_fn` / `ordered_sum` inject CPU checkers in tests.
     """
 
     def __init__(self, n_agents: int, P: int, rho: float = 0.1, lr: float = 0.1, momentum: float = 0.5,
                  local_steps: int = 1, frac: float = 1.0, seed: int = 2028, device=None, mean: str = "exact",
-                 group=None, metrics: bool = True, round_fn=None, ordered_sum=None, fused: Optional[bool] = None):
+                 group=None, metrics: bool = True, round_fn=None, ordered_sum=None, fused: Optional[bool] = None,
+                 shard: str = "agents"):
         import numpy as np
         import torch.distributed as dist
 
@@ -123,13 +134,24 @@ class SeparableADMM:
         from .bank import row_stride
         if mean not in ("exact", "fast"):
             raise ValueError("mean must be 'exact' or 'fast'")
+        if shard not in ("agents", "columns"):
+            raise ValueError("shard must be 'agents' or 'columns'")
+        self.shard = shard
         self.N, self.P = int(n_agents), int(P)
         self.rho, self.lr, self.mu, self.local_steps = float(rho), float(lr), float(momentum), int(local_steps)
         self.m = max(int(frac * self.N), 1)
         self.mean_mode, self.group, self.metrics = mean, group, metrics
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
-        self.lo, self.hi = parallel.shard_bounds(self.N, self.world, self.rank)
+        if shard == "columns":
+            # every agent, this rank's parameter columns [c0, c1): the kernels see Pl columns
+            self.lo, self.hi = 0, self.N
+            self.c0, self.c1 = parallel.column_bounds(self.P, self.world, self.rank)
+            mean = self.mean_mode = "exact"  # each column block's mean IS the reference's order
+        else:
+            self.lo, self.hi = parallel.shard_bounds(self.N, self.world, self.rank)
+            self.c0, self.c1 = 0, self.P
+        self.Pl = self.c1 - self.c0
         self.n = self.hi - self.lo
         self.device = torch.device(device) if device is not None else torch.device("cuda")
         self._round = round_fn if round_fn is not None else ops.admm_ls_round
@@ -142,22 +164,31 @@ class SeparableADMM:
         if fused is None:
             fused = os.environ.get("DOL_ADMM_FUSED_MEAN", "1") != "0"
         self.fused = bool(fused) and round_fn is None and ordered_sum is None and \
-            (self.world == 1 or mean == "fast")
+            (self.world == 1 or mean == "fast" or shard == "columns")
         self._round_mean = ops.admm_ls_round_mean
         self._parallel = parallel
         self.rs = np.random.RandomState(seed)  # the reference's np.random.choice stream (setup_seed)
-        ld = row_stride(self.P)
+        ld = row_stride(max(self.Pl, 1))
         dev = self.device
         self.w = torch.zeros(max(self.n, 1), ld, dtype=torch.float32, device=dev)
         self.alpha = torch.zeros_like(self.w)
         self.target = torch.empty_like(self.w)
         self.mom = torch.zeros_like(self.w) if self.mu != 0.0 else None
-        for k in range(self.lo, self.hi):  # per-row seeds: identical rows for every sharding
+        # per-row seeds over the whole row: identical rows (and column blocks) for every sharding
+        full_row = torch.empty(self.P, dtype=torch.float32, device=dev) if shard == "columns" else None
+        for k in range(self.lo, self.hi):
             g = torch.Generator(device=dev).manual_seed(seed * 1000003 + k + 1)
-            self.target[k - self.lo, :self.P].normal_(generator=g)
+            if full_row is None:
+                self.target[k - self.lo, :self.P].normal_(generator=g)
+            else:
+                full_row.normal_(generator=g)
+                self.target[k - self.lo, :self.Pl].copy_(full_row[self.c0:self.c1])
+        del full_row
         g = torch.Generator(device=dev).manual_seed(seed)
         self.theta = torch.zeros(ld, dtype=torch.float32, device=dev)
-        self.theta[:self.P].normal_(generator=g)
+        th = torch.empty(self.P, dtype=torch.float32, device=dev).normal_(generator=g)
+        self.theta[:self.Pl].copy_(th[self.c0:self.c1])
+        del th
         self.theta0 = self.theta.clone()
         self._theta_next = torch.zeros_like(self.theta)
         self.mom_started = np.zeros(max(self.n, 1), dtype=bool)
@@ -178,6 +209,8 @@ class SeparableADMM:
         dev = self.device
         ml = len(local)
         rw = ra = None
+        if self.shard == "columns":
+            return self._column_round(order)
         if self.fused:
             return self._fused_round(order, local)
         if ml:
@@ -207,15 +240,73 @@ class SeparableADMM:
                 s[0] = rw.sum()
                 s[1] = ra.sum()
             if self.world > 1:
-                import torch.distributed as dist
-                if s.device.type == "cuda" and dist.get_backend(self.group) == "gloo":
-                    h = s.cpu()
-                    dist.all_reduce(h, group=self.group)
-                    s.copy_(h)
-                else:
-                    dist.all_reduce(s, group=self.group)
+                self._all_reduce(s)
             self._pending.append((self.rounds, s))
         self.rounds += 1
+
+    def _all_reduce(self, s: torch.Tensor) -> torch.Tensor:
+        """all_reduce(SUM) in place (gloo: device tensors staged through host memory)."""
+        import torch.distributed as dist
+        if s.device.type == "cuda" and self._parallel._backend(self.group) == "gloo":
+            h = s.cpu()
+            dist.all_reduce(h, group=self.group)
+            s.copy_(h)
+        else:
+            dist.all_reduce(s, group=self.group)
+        return s
+
+    def _column_round(self, order) -> None:
+        """shard="columns": every sampled agent's client round and the server's
+        ordered mean on this rank's parameter columns, in the global sampled
+        order, with no collective (the round and the mean of DEC/servers.py:
+        50-81 are per coordinate; theta's block is the reference's bits)."""
+        dev = self.device
+        m = int(order.size)
+        s = torch.zeros(2, dtype=torch.float64, device=dev) if self.metrics else None
+        if self.Pl > 0:
+            rows = torch.as_tensor(order, dtype=torch.int32, device=dev)
+            first = None
+            if self.mom is not None:
+                first = torch.as_tensor(~self.mom_started[order], dtype=torch.int32, device=dev)
+            if self.fused:
+                self._round_mean(self.w, self.alpha, self.target, self.theta, agents=rows, first=first, buf=self.mom,
+                                 rho=self.rho, lr=self.lr, momentum=self.mu, local_steps=self.local_steps,
+                                 out=self._theta_next, scale=float(m), resid_total=s, P=self.Pl, validate=False)
+            else:  # two passes (injected checkers / DOL_ADMM_FUSED_MEAN=0): the client round, then the ordered mean
+                rw = ra = None
+                if self.metrics:
+                    rw = torch.empty(m, dtype=torch.float64, device=dev)
+                    ra = torch.empty(m, dtype=torch.float64, device=dev)
+                self._round(self.w, self.alpha, self.target, self.theta, agents=rows, first=first, buf=self.mom,
+                            rho=self.rho, lr=self.lr, momentum=self.mu, local_steps=self.local_steps, resid_sq=rw,
+                            alpha_sq=ra, P=self.Pl)
+                self._osum(self.w, rows, out=self._theta_next, scale=float(m), P=self.Pl)
+                if self.metrics:
+                    s[0] = rw.sum()
+                    s[1] = ra.sum()
+        if self.mom is not None and self.local_steps > 0:
+            self.mom_started[order] = True
+        self.theta, self._theta_next = self._theta_next, self.theta
+        if self.metrics:
+            self._pending.append((self.rounds, s))  # this rank's columns only: summed in `history`
+        self.rounds += 1
+
+    def full_theta(self) -> torch.Tensor:
+        """theta over all P columns on every rank (shard="columns": one
+        all_gather of the column blocks; diagnostics and checkpoints, not on the
+        round path)."""
+        if self.shard != "columns" or self.world == 1:
+            return self.theta[:self.P]
+        return self._gather_columns(self.theta[:self.Pl])
+
+    def _gather_columns(self, v: torch.Tensor) -> torch.Tensor:
+        par = self._parallel
+        bounds = [par.column_bounds(self.P, self.world, q) for q in range(self.world)]
+        width = max(max(b - a for a, b in bounds), 1)
+        pad = torch.zeros(width, dtype=v.dtype, device=v.device)
+        pad[:v.numel()] = v
+        parts = par._all_gather(pad, self.group)
+        return torch.cat([parts[q][:b - a] for q, (a, b) in enumerate(bounds)])
 
     def _fused_round(self, order, local) -> None:
         """round() on dol_admm_ls_round_mean_f32: the client round and this
@@ -235,7 +326,7 @@ class SeparableADMM:
             self._round_mean(self.w, self.alpha, self.target, self.theta, agents=rows, first=first, buf=self.mom,
                              rho=self.rho, lr=self.lr, momentum=self.mu, local_steps=self.local_steps,
                              out=self._theta_next, scale=float(self.m) if self.world == 1 else 1.0,
-                             resid_total=s, P=self.P)
+                             resid_total=s, P=self.P, validate=False)
             if self.mom is not None and self.local_steps > 0:
                 self.mom_started[local] = True
         else:  # a rank without sampled rows ('fast' mean): contributes zeros
@@ -245,50 +336,50 @@ class SeparableADMM:
         self.theta, self._theta_next = self._theta_next, self.theta
         if self.metrics:
             if self.world > 1:
-                import torch.distributed as dist
-                if s.device.type == "cuda" and dist.get_backend(self.group) == "gloo":
-                    h = s.cpu()
-                    dist.all_reduce(h, group=self.group)
-                    s.copy_(h)
-                else:
-                    dist.all_reduce(s, group=self.group)
+                self._all_reduce(s)
             self._pending.append((self.rounds, s))
         self.rounds += 1
 
     @property
     def history(self):
-        """Per-round metrics: {"round", "primal_resid_sq", "dual_sq"} (sums over the sampled clients)."""
-        for r, s in self._pending:
-            v = s.cpu().tolist()
-            self._history.append({"round": r, "primal_resid_sq": v[0], "dual_sq": v[1]})
+        """Per-round metrics: {"round", "primal_resid_sq", "dual_sq"} (sums over
+        the sampled clients).  shard="columns" at world > 1: the pending
+        per-rank partials are summed across ranks here, in one all_reduce --
+        every rank must read `history` at the same point."""
+        if self._pending:
+            if self.shard == "columns" and self.world > 1:
+                stacked = self._all_reduce(torch.stack([s for _, s in self._pending]))
+                self._pending = [(r, stacked[i]) for i, (r, _) in enumerate(self._pending)]
+            for r, s in self._pending:
+                v = s.cpu().tolist()
+                self._history.append({"round": r, "primal_resid_sq": v[0], "dual_sq": v[1]})
         self._pending = []
         return self._history
 
     def optimum(self) -> torch.Tensor:
         """mean_k t_k in fp64 (the minimiser of sum_k f_k); all ranks (diagnostic)."""
+        if self.shard == "columns":
+            s = self.target[:self.n, :self.Pl].double().sum(0)
+            return (s if self.world == 1 else self._gather_columns(s)) / self.N
         s = self.target[:self.n, :self.P].double().sum(0)
         if self.world > 1:
-            import torch.distributed as dist
-            if s.device.type == "cuda" and dist.get_backend(self.group) == "gloo":
-                h = s.cpu()
-                dist.all_reduce(h, group=self.group)
-                s.copy_(h)
-            else:
-                dist.all_reduce(s, group=self.group)
+            self._all_reduce(s)
         return s / self.N
 
     def distance_to_optimum(self) -> float:
         """||theta - mean_k t_k|| / sqrt(P)."""
-        return float((self.theta[:self.P].double() - self.optimum()).norm() / self.P ** 0.5)
+        return float((self.full_theta().double() - self.optimum()).norm() / self.P ** 0.5)
 
     def fixed_point(self) -> torch.Tensor:
         """theta* = (mean_k t_k + rho*theta_0) / (1 + rho): where the reference's
         iteration settles under full participation (see the class docstring)."""
-        return (self.optimum() + self.rho * self.theta0[:self.P].double()) / (1.0 + self.rho)
+        theta0 = self.theta0[:self.P] if self.shard != "columns" or self.world == 1 else \
+            self._gather_columns(self.theta0[:self.Pl])
+        return (self.optimum() + self.rho * theta0.double()) / (1.0 + self.rho)
 
     def distance_to_fixed_point(self) -> float:
         """||theta - theta*|| / sqrt(P) (full participation)."""
-        return float((self.theta[:self.P].double() - self.fixed_point()).norm() / self.P ** 0.5)
+        return float((self.full_theta().double() - self.fixed_point()).norm() / self.P ** 0.5)
 
 
 class SeparableDGDPM:

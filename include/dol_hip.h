@@ -34,6 +34,9 @@ extern "C" {
 
 #define DOL_OK 0
 #define DOL_EINVAL (-1)
+/* dol_bank_alloc only: the retired-address-space cap would be exceeded (outside
+ * the -(hipError_t) range). */
+#define DOL_ECAP (-100000)
 
 /* Library version, e.g. 100 for 0.1.0. */
 int dol_version(void);
@@ -475,18 +478,28 @@ int dol_er_stochastic_f32(float* W, int64_t ldw, int32_t n, float p, uint64_t se
  * Device memory for a bank buffer as ONE physical allocation (hipMemCreate)
  * mapped into a reserved virtual range (hipMemAddressReserve + hipMemMap),
  * rounded up to the allocation granularity (*mapped_bytes).  Free with
- * dol_bank_free(ptr, *mapped_bytes), which unmaps the range, frees it and
- * then releases the physical allocation, with the size recorded at allocation;
- * it refuses a pointer this library did not hand out or a size other than
- * *mapped_bytes (DOL_EINVAL, before any HIP call) and accepts NULL.  A failed
- * step leaves the block registered: calling dol_bank_free again resumes at
- * that step.  Host-side,
- * synchronous, thread-safe, not graph-capturable.  Opt-in for bank buffers
- * (bank.device_matrix, DOL_BANK_ALLOC=vmm).  No reference counterpart (the
- * reference keeps one nn.Module per agent in host memory).
+ * dol_bank_free(ptr, *mapped_bytes), with the size recorded at allocation: it
+ * unmaps the range and releases the physical allocation, and RETIRES the
+ * virtual range (keeps it reserved, never reused: on this ROCm stack a range
+ * re-mapped after a free was read through stale translations)
+ * unless DOL_BANK_FREE_VA=1 (diagnostics: the range is freed).  Retired bytes
+ * are counted (dol_bank_retired_bytes / _blocks); dol_bank_alloc returns
+ * DOL_ECAP when retired + live mapped + the new block would pass
+ * dol_bank_retired_cap_bytes() (DOL_BANK_RETIRED_VA_CAP_GIB, default 4096).
+ * dol_bank_free refuses a pointer this library did not hand out or a size
+ * other than *mapped_bytes (DOL_EINVAL, before any HIP call) and accepts NULL.
+ * A failed step leaves the block registered: calling dol_bank_free again
+ * resumes at that step.  Host-side, synchronous, thread-safe, not
+ * graph-capturable.  The default for bank matrices of >= 1 GiB
+ * (bank.device_matrix); DOL_BANK_ALLOC=torch or mapped=False opts out.  No
+ * reference counterpart (the reference keeps one nn.Module per agent in host
+ * memory).
  */
 int dol_bank_alloc(int64_t bytes, void** ptr, int64_t* mapped_bytes);
 int dol_bank_free(void* ptr, int64_t mapped_bytes);
+int64_t dol_bank_retired_bytes(void);
+int64_t dol_bank_retired_blocks(void);
+int64_t dol_bank_retired_cap_bytes(void);
 
 /* Streaming copy dst = src (n floats): HBM calibration kernel for roofline. */
 int dol_stream_copy_f32(const float* src, float* dst, int64_t n, hipStream_t s);

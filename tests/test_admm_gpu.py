@@ -205,6 +205,12 @@ def test_admm_ls_round_mean_argument_errors(gpu):
         ops.admm_ls_round_mean(w, w.clone(), w.clone(), th, resid_total=torch.zeros(1, dtype=torch.float64, device=gpu))
     with pytest.raises(ValueError, match="at least one"):
         ops.admm_ls_round_mean(w, w.clone(), w.clone(), th, agents=torch.zeros(0, dtype=torch.int32, device=gpu))
+    # the kernel prefetches the next agents' rows before storing the
+    # current ones, so repeated or out-of-range ids are refused on the host
+    for bad in ([1, 2, 1], [0, 4], [-1, 0], [0, 1, 2, 3, 0]):
+        with pytest.raises(ValueError, match="agents"):
+            ops.admm_ls_round_mean(w, w.clone(), w.clone(), th,
+                                   agents=torch.tensor(bad, dtype=torch.int32, device=gpu))
 
 
 def test_admm_ls_round_mean_defaults_and_no_metrics(gpu):

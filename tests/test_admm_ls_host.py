@@ -170,6 +170,86 @@ def test_sharded_admm_matches_single_process(world, mean):
         assert bits_equal(a, ref.alpha[:N, :P].numpy())
 
 
+def _column_worker(rank, world, port, N, P, rounds, kw, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    parallel.init_process_group("gloo", rank=rank, world_size=world, timeout_s=120)
+    try:
+        from dolhip.synthetic import SeparableADMM
+        calls = []
+        real_all_reduce, real_all_gather = dist.all_reduce, dist.all_gather_into_tensor
+
+        def counting(fn, name):
+            def wrapped(*a, **k):
+                calls.append(name)
+                return fn(*a, **k)
+            return wrapped
+        s = SeparableADMM(N, P, device="cpu", round_fn=cpu_admm_ls_round, ordered_sum=cpu_ordered_sum,
+                          shard="columns", **kw)
+        # the round path: no collective at all
+        dist.all_reduce = counting(real_all_reduce, "all_reduce")
+        dist.all_gather_into_tensor = counting(real_all_gather, "all_gather")
+        try:
+            for _ in range(rounds):
+                s.round()
+            n_round_calls = len(calls)
+        finally:
+            dist.all_reduce, dist.all_gather_into_tensor = real_all_reduce, real_all_gather
+        theta = s.full_theta().numpy().copy()
+        hist = [(h["primal_resid_sq"], h["dual_sq"]) for h in s.history]
+        q.put((rank, s.c0, s.c1, s.w[:N, :s.Pl].numpy().copy(), s.alpha[:N, :s.Pl].numpy().copy(), theta, hist,
+               n_round_calls, s.distance_to_fixed_point()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,P", [(2, 300), (3, 300), (8, 600), (8, 65)])
+def test_column_sharded_admm_matches_single_process(world, P):
+    """SeparableADMM(shard="columns") -- every rank runs
+    all sampled agents on its parameter columns, in the global sampled order
+    -- is bit-identical to one process (rows, duals and theta; theta is
+    DEC/servers.py:42-48's order exactly) with no collective on the round path;
+    ranks without columns (P = 65 over 8) take part; the residual metrics
+    (per-rank partials summed when `history` is read) agree to fp64 rounding."""
+    N, rounds = 13, 4
+    ref = _run(N, P, rounds, "exact", **KW)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_column_worker, args=(r, world, port, N, P, rounds, KW, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [r[1] for r in res] == [parallel.column_bounds(P, world, k)[0] for k in range(world)]
+    w = np.concatenate([r[3] for r in res], axis=1)
+    a = np.concatenate([r[4] for r in res], axis=1)
+    assert bits_equal(w, ref.w[:N, :P].numpy())
+    assert bits_equal(a, ref.alpha[:N, :P].numpy())
+    hist = [(h["primal_resid_sq"], h["dual_sq"]) for h in ref.history]
+    for r in res:
+        assert bits_equal(r[5], ref.theta[:P].numpy())
+        np.testing.assert_allclose(np.array(r[6]), np.array(hist), rtol=1e-12)
+        assert r[7] == 0, f"rank {r[0]}: {r[7]} collectives on the round path"
+        assert r[8] == pytest.approx(ref.distance_to_fixed_point(), rel=1e-9)
+
+
+def test_column_sharded_admm_one_process_is_the_agent_path():
+    """shard="columns" at world 1 is the plain one-process problem (same bits)."""
+    from dolhip.synthetic import SeparableADMM
+    a = _run(11, 70, 3, "exact", **KW)
+    b = SeparableADMM(11, 70, device="cpu", round_fn=cpu_admm_ls_round, ordered_sum=cpu_ordered_sum, shard="columns",
+                      **KW)
+    for _ in range(3):
+        b.round()
+    assert bits_equal(b.theta[:70].numpy(), a.theta[:70].numpy())
+    assert bits_equal(b.w[:11, :70].numpy(), a.w[:11, :70].numpy())
+    with pytest.raises(ValueError):
+        SeparableADMM(4, 8, device="cpu", round_fn=cpu_admm_ls_round, ordered_sum=cpu_ordered_sum, shard="rows")
+
+
 def test_separable_admm_converges_to_reference_fixed_point():
     """Full participation: theta -> (mean t + rho theta_0) / (1 + rho), the fixed
     point of the reference's iteration (its server averages w only), NOT mean t;

@@ -177,3 +177,114 @@ def test_fused_pass_destination_check_replaces_a_slow_pair(gpu, monkeypatch):
     for _ in range(15):
         want = oracle.mix_ring(want, wp, wn)
     assert bits_equal(got, want)
+
+
+def _ring_bank(gpu, monkeypatch, n=96, P=1000, alloc="torch"):
+    from dolhip import graph as G
+    monkeypatch.setattr(B, "PAIR_PROBE_MIN_BYTES", 0)
+    monkeypatch.setenv("DOL_BANK_PAIR_PROBE", "1")
+    monkeypatch.setenv("DOL_BANK_ALLOC", alloc)
+    plan = G.MixingPlan(G.communication_csr("circle", "stochastic", n)[0], gpu)
+    bank = B.AgentBank(n, P, gpu)
+    bank.rows().copy_(torch.from_numpy(np.random.default_rng(5).standard_normal((n, P)).astype(np.float32)).to(gpu))
+    return bank, plan
+
+
+def test_destination_check_probes_at_the_calibrated_step_count(gpu, monkeypatch):
+    """a longer fused pass carries more arithmetic per byte, so its
+    pass / round ratio rises with the step count.  The check times the pair
+    at PAIR_PROBE_STEPS (the count PAIR_RATIO was calibrated on) whatever the
+    pass's own count: with a timer whose ratio is 1 + 0.02 * steps, mix(steps
+    = 8) keeps its buffers (1.10 at 5 rounds; 1.16 at 8 would read as slow)."""
+    bank, plan = _ring_bank(gpu, monkeypatch)
+    seen = []
+
+    def timer(x, y, plan_, steps, P_):
+        seen.append(steps)
+        return 1.0 + 0.02 * steps, 1.0
+    bank._pair_timer = timer
+    y0, x0 = bank.buffer("y").data_ptr(), bank.buffer("x").data_ptr()
+    bank.mix(plan, steps=8)
+    bank.mix(plan, steps=16)
+    torch.cuda.synchronize()
+    assert seen == [B.PAIR_PROBE_STEPS, B.PAIR_PROBE_STEPS]  # each direction once, at the calibrated count
+    assert {bank.x.data_ptr(), bank.buffer("y").data_ptr()} == {x0, y0}
+    assert all(p["steps"] == B.PAIR_PROBE_STEPS and p["attempt"] == 0 for p in bank.pair_probes)
+
+
+def test_destination_check_holds_one_candidate_and_stops_on_a_reused_block(gpu, monkeypatch):
+    """Every pair reads slow: the losing candidate is dropped before the next
+    allocation (at most one buffer besides the best is held), and when torch's
+    caching allocator hands the dropped block straight back the search stops
+    instead of re-measuring it."""
+    bank, plan = _ring_bank(gpu, monkeypatch)
+    nbytes = bank.n * bank.ld * 4
+    bank._pair_timer = lambda x, y, p, steps, P_: (2.0, 1.0)
+    y0 = bank.buffer("y").data_ptr()
+    torch.cuda.synchronize()
+    base = torch.cuda.memory_allocated(gpu)
+    torch.cuda.reset_peak_memory_stats(gpu)
+    bank.mix(plan, steps=5)
+    torch.cuda.synchronize()
+    peak = torch.cuda.max_memory_allocated(gpu) - base
+    assert peak <= nbytes + (4 << 20)  # the best so far + ONE fresh candidate, never two
+    probes = bank.pair_probes
+    assert [p["attempt"] for p in probes] == [0, 1] and probes[-1].get("same_block")
+    assert bank.x.data_ptr() == y0  # the first (equally slow) destination was kept and written
+
+
+def test_destination_check_keeps_adopted_buffers(gpu, monkeypatch):
+    """Buffers handed in with adopt() stay the caller's: a slow pair is
+    recorded, not replaced -- unless adopted with replaceable=True."""
+    bank, plan = _ring_bank(gpu, monkeypatch)
+    bank._pair_timer = lambda x, y, p, steps, P_: (2.0, 1.0)
+    mine = torch.empty_like(bank.buffer("y"))
+    bank.adopt("y", mine)
+    bank.mix(plan, steps=5)
+    assert bank.x.data_ptr() == mine.data_ptr()
+    assert bank.pair_probes[-1].get("kept_adopted") and len(bank.pair_probes) == 1
+    bank2, plan2 = _ring_bank(gpu, monkeypatch)
+    bank2._pair_timer = lambda x, y, p, steps, P_: (2.0, 1.0)
+    mine2 = torch.empty_like(bank2.buffer("y"))
+    bank2.adopt("y", mine2, replaceable=True)
+    bank2.mix(plan2, steps=5)
+    assert len(bank2.pair_probes) >= 2  # replaced and re-timed
+    torch.cuda.synchronize()
+
+
+def test_retired_address_space_is_counted_and_capped(gpu, monkeypatch):
+    """ADVICE r05 / VERDICT r05 item 8: dol_bank_free retires the virtual range
+    of a mapped block; the retired bytes are counted through the C-ABI, and
+    past DOL_BANK_RETIRED_VA_CAP_GIB dol_bank_alloc refuses (DOL_ECAP):
+    mapped=True raises, the default falls back to torch's allocator with a
+    warning.  200 map/free cycles keep the process working."""
+    from dolhip._native import DolNativeError
+    monkeypatch.setattr(B, "MAPPED_MIN_BYTES", 0)
+    monkeypatch.delenv("DOL_BANK_ALLOC", raising=False)
+    monkeypatch.delenv("DOL_BANK_RETIRED_VA_CAP_GIB", raising=False)
+    before = B.retired_va()
+    for k in range(200):
+        X = B.device_matrix(64, 8192, gpu, mapped=True)  # 2 MiB
+        X.fill_(float(k))
+        assert float(X[63, 8191]) == float(k)
+        del X
+        gc.collect()
+    torch.cuda.synchronize()
+    after = B.retired_va()
+    assert after["blocks"] == before["blocks"] + 200
+    assert after["bytes"] >= before["bytes"] + 200 * 64 * 8192 * 4
+    assert after["cap_bytes"] == 4096 << 30
+    monkeypatch.setenv("DOL_BANK_RETIRED_VA_CAP_GIB", "0")  # a cap below what is already retired
+    assert B.retired_va()["cap_bytes"] == 0
+    with pytest.raises(DolNativeError, match="DOL_BANK_RETIRED_VA_CAP_GIB"):
+        B.device_matrix(64, 8192, gpu, mapped=True)
+    monkeypatch.setattr(B, "_CAP_WARNED", [])
+    with pytest.warns(ResourceWarning):
+        t = B.device_matrix(64, 8192, gpu)  # default: torch's allocator instead
+    t.fill_(1.0)
+    assert float(t.sum()) == 64 * 8192
+    monkeypatch.delenv("DOL_BANK_RETIRED_VA_CAP_GIB")
+    X = B.device_matrix(64, 8192, gpu, mapped=True)
+    del X, t
+    gc.collect()
+    torch.cuda.synchronize()

@@ -475,3 +475,187 @@ def test_stalled_rank_raises_within_timeout(what):
     status, elapsed = res[0]
     assert status != "returned", f"{what}: rank 0 returned although its peer never took part"
     assert elapsed < 3 * timeout_s, f"{what}: raised only after {elapsed:.1f} s (timeout {timeout_s} s)"
+
+
+# ---------------------------------------------------------------------------
+# every line RCCL would run, executed on the CPU tier
+# ---------------------------------------------------------------------------
+
+def cpu_dgd_ring_edges(X, Y, w_prev, w_next, target, halo_prev, halo_next, mom=None, P=None, n_rows=None, **kw):
+    """CPU stand-in for dol_dgd_ring_edges_f32: rows 0 and n-1 of the block."""
+    n = X.shape[0] if n_rows is None else n_rows
+    m0 = None if mom is None else mom[0:1]
+    cpu_dgd_ring(X[0:1], Y[0:1], w_prev[0:1], w_next[0:1], target[0:1], mom=m0, halo_prev=halo_prev,
+                 halo_next=X[1] if n > 1 else halo_next, P=P, n_rows=1, **kw)
+    if n > 1:
+        m1 = None if mom is None else mom[n - 1:n]
+        cpu_dgd_ring(X[n - 1:n], Y[n - 1:n], w_prev[n - 1:n], w_next[n - 1:n], target[n - 1:n], mom=m1,
+                     halo_prev=X[n - 2], halo_next=halo_next, P=P, n_rows=1, **kw)
+    return Y
+
+
+class _FakeEvent:
+    def record(self, *a):
+        pass
+
+
+def _line_tracer(path, hits):
+    import sys
+
+    def local(frame, event, arg):
+        if event == "line":
+            hits.add(frame.f_lineno)
+        return local
+
+    def glob(frame, event, arg):
+        if frame.f_code.co_filename == path:
+            return local
+        return None
+    sys.settrace(glob)
+
+
+def _exercise_parallel(world, rank):
+    """Every entry of dolhip.parallel on CPU tensors: ring (mix + DGD, with and
+    without the one-launch edge entries), column sharding (+ set_plan, gather),
+    the agent/column transpose (direct and staged-copy blocks, the piecewise
+    overlapped form), the fast and exact means (a rank with and without
+    sampled rows, host and tensor orders)."""
+    from types import SimpleNamespace
+    N, P = 11, 130
+    rng = np.random.default_rng(3)
+    X = rng.standard_normal((N, P)).astype(np.float32)
+    wp, wn = rng.random(N).astype(np.float32), rng.random(N).astype(np.float32)
+    for edges in (True, False):
+        ring = parallel.ShardedRing(N, P, wp, wn, "cpu", ld=P + 2, mix_ring=cpu_mix_ring, dgd_ring=cpu_dgd_ring,
+                                    mix_edges=cpu_mix_ring_edges if edges else None,
+                                    dgd_edges=cpu_dgd_ring_edges if edges else None)
+        ring.x[:, :P] = torch.from_numpy(X[ring.lo:ring.hi])
+        ring.kernel_events = (_FakeEvent(), _FakeEvent())
+        ring.step()
+        ring.step(ring.x, ring.y)
+        t = torch.from_numpy(X[ring.lo:ring.hi].copy())
+        ring.dgd_step(t, mom=torch.zeros_like(t), steps=1, lr=0.1, momentum=0.5, first_step=True)
+        ring.dgd_step(t, steps=1, lr=0.1)
+    csr = _er_csr(N, 0.4, seed=1)
+    plan = SimpleNamespace(n_rows=N, n_cols=N, apply=cpu_apply_csr(csr), apply_dgd=cpu_apply_dgd(csr))
+    sh = parallel.ColumnSharded(plan, P, "cpu")
+    sh.x[:, :sh.Pl] = torch.from_numpy(np.ascontiguousarray(X[:, sh.c0:sh.c1]))
+    sh.step()
+    sh.dgd_step(torch.from_numpy(np.ascontiguousarray(X[:, sh.c0:sh.c1])), steps=1, lr=0.1)
+    sh.set_plan(plan)
+    sh.set_plan(plan, apply=cpu_apply_csr(csr))
+    sh.local_cols(torch.zeros(N, P))
+    sh.gather(0)
+    tr = parallel.AgentColumnTranspose(N, P, "cpu")
+    tr.set_plan(plan)
+    rows = torch.from_numpy(np.ascontiguousarray(X[tr.lo:tr.hi]))
+    tr.mix(rows)
+    tr.to_columns(rows)
+    tr.cols_out.copy_(tr.cols)
+    tr.from_columns(rows)
+    tr.mix_with_local_steps(rows, lambda a, b: rows[a:b].mul_(0.5), chunks=2, out=rows.clone(),
+                            before_mix=lambda: None)
+    tr.mix_with_local_steps(rows, lambda a, b: None, chunks=1)
+    parallel.AgentColumnTranspose(N, P, "cpu", apply=cpu_apply_csr(csr)).mix(rows)  # an injected block mix
+    Xl = torch.zeros(max(tr.n_local, 1), P + 3)
+    Xl[:tr.n_local, :P] = torch.from_numpy(X[tr.lo:tr.hi])
+    for order in ([0, N - 1, 5, 2], [N - 1]):  # rank 0 has no sampled row in the second
+        local = [g - tr.lo for g in order if tr.lo <= g < tr.hi]
+        parallel.global_mean(Xl, local, len(order), P, ordered_sum=cpu_ordered_sum)
+        parallel.global_mean(Xl, torch.tensor(local, dtype=torch.int32), len(order), P, ordered_sum=cpu_ordered_sum)
+        parallel.global_mean_exact(Xl, tr.lo, tr.hi, order, P, ordered_sum=cpu_ordered_sum)
+
+
+def _coverage_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    parallel.init_process_group("gloo", rank=rank, world_size=world, timeout_s=120)
+    hits = set()
+    try:
+        # every backend-dependent branch answers as it would over RCCL; the
+        # transport underneath stays gloo (CPU tensors: nothing is staged)
+        real_backend = parallel._backend
+        parallel._backend = lambda group=None: (real_backend(group), "nccl")[1]
+        _line_tracer(parallel.__file__, hits)
+        _exercise_parallel(world, rank)
+    finally:
+        import sys
+        sys.settrace(None)
+        q.put((rank, sorted(hits)))
+        dist.destroy_process_group()
+
+
+def _parallel_lines_rccl_runs():
+    """Line numbers of the statements in dolhip/parallel.py's functions, minus
+    the ones RCCL never runs: host staging for gloo (`# staged`), gloo's
+    bounded host wait (`# gloo-only`), raises (error paths) and docstrings.
+    `# device-only` lines (CUDA events / side streams) need a GPU and run in
+    tests/test_parallel_gpu.py; they are returned separately."""
+    import ast
+    src = open(parallel.__file__).read()
+    text = src.splitlines()
+    want, device = set(), set()
+    for fn in ast.walk(ast.parse(src)):
+        if not isinstance(fn, (ast.FunctionDef, ast.AsyncFunctionDef)):
+            continue
+        body = fn.body
+        if body and isinstance(body[0], ast.Expr) and isinstance(getattr(body[0], "value", None), ast.Constant):
+            body = body[1:]
+        for stmt in body:
+            for node in ast.walk(stmt):
+                if not isinstance(node, ast.stmt) or isinstance(node, (ast.FunctionDef, ast.AsyncFunctionDef)):
+                    continue
+                line = text[node.lineno - 1]
+                if isinstance(node, ast.Raise) or "# staged" in line or "# gloo-only" in line:
+                    continue
+                (device if "# device-only" in line else want).add(node.lineno)
+    return want, device
+
+
+def test_every_rccl_line_runs_under_gloo():
+    """the branches only RCCL takes (unstaged device
+    tensors through send/recv, all_to_all and all_reduce, the
+    all_gather_into_tensor gather, stream-side waits) execute here: gloo
+    ranks of CPU tensors with parallel._backend answering "nccl", every entry
+    of dolhip.parallel called at world 2 and 3 (plus world 1 and the nccl
+    set-up of init_process_group in this process), and every statement RCCL
+    would run is hit."""
+    import sys
+    want, device = _parallel_lines_rccl_runs()
+    hits = set()
+    for world in (2, 3):
+        ctx = mp.get_context("spawn")
+        q = ctx.Queue()
+        port = _free_port()
+        procs = [ctx.Process(target=_coverage_worker, args=(r, world, port, q)) for r in range(world)]
+        for p in procs:
+            p.start()
+        for _ in range(world):
+            hits.update(q.get(timeout=180)[1])
+        for p in procs:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+    # world 1 (no process group) and init_process_group's RCCL set-up (recorded, not run)
+    local = set()
+    seen = {}
+    real_init = dist.init_process_group
+    saved_env = os.environ.get("TORCH_NCCL_ASYNC_ERROR_HANDLING")
+    dist.init_process_group = lambda backend, **kw: seen.update(backend=backend, **kw)
+    _line_tracer(parallel.__file__, local)
+    try:
+        parallel.init_process_group("nccl", rank=0, world_size=1, device="cpu", timeout_s=5)
+        _exercise_parallel(1, 0)
+    finally:
+        sys.settrace(None)
+        dist.init_process_group = real_init
+        if saved_env is None:
+            os.environ.pop("TORCH_NCCL_ASYNC_ERROR_HANDLING", None)
+        else:
+            os.environ["TORCH_NCCL_ASYNC_ERROR_HANDLING"] = saved_env
+    assert seen["backend"] == "nccl" and str(seen["device_id"]) == "cpu" and seen["world_size"] == 1
+    hits |= local
+    missing = sorted(want - hits)
+    text = open(parallel.__file__).read().splitlines()
+    assert not missing, "lines RCCL runs that no CPU test executed:\n" + "\n".join(
+        f"{n}: {text[n - 1].strip()}" for n in missing)
+    assert device and not (device & hits)  # the device-only lines really are (no CUDA here)
