@@ -43,6 +43,7 @@
 // XCD's L2 for the others.
 #include <hip/hip_runtime.h>
 #include <algorithm>
+#include <atomic>
 #include <stdint.h>
 #include <stdlib.h>
 
@@ -135,7 +136,19 @@ __device__ __forceinline__ uint32_t piece_addr(uint32_t o, uint32_t lb) { return
 // item.  Persistent (G < n_items): the chunk stream runs on across items — the
 // next item's chunk 0 is staged during the current item's last chunk, so a new
 // item does not start on an exposed DMA latency (needs nk >= 2).
-template <int PROBE = 0, bool A4 = false>
+// STREAM (r06, dol_slab_set_variant(2)): each wave walks its run of entry
+// pairs for the chunk as ONE software-pipelined stream instead of a loop per
+// row: the index pair two steps ahead and the gathers one step ahead are in
+// flight while a pair is summed (registers rotate through a 6-step unrolled
+// body, so no copies), and the running sum `a` moves between the wave's 8 row
+// accumulators -- one 32-register tuple -- only at a row boundary, by
+// dynamically indexed register moves (s_set_gpr_idx_on: 4 moves out, 4 in).
+// Per pair: one uniform compare for the boundary; the r03 loop paid a loop
+// entry, tail cases and a prefetch per (row, chunk) segment (~30 instructions
+// per 6.4-entry segment).  Same entries, same order, same bits.  Reads run at
+// most two pairs past the wave's run (kAhead): the index DMA covers them and
+// the packer pads past the last block (slab_tail_kernel).
+template <int PROBE = 0, bool A4 = false, bool STREAM = false>
 __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
     const float* __restrict__ X, int64_t ldx, int x_rows, float* __restrict__ Y, int64_t ldy, int n_rows, int64_t P,
     const int32_t* __restrict__ ent, const int32_t* __restrict__ hdr, int nk, int n_rg, int64_t n_slabs,
@@ -202,7 +215,7 @@ __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
     const int64_t a0 = int64_t(blk0 & ~1) * 8;  // even: 16-B aligned
     const int64_t nbytes = int64_t(blk1 & ~1) * 8 - a0;
     if (nbytes <= kIdxBytes - kAhead)
-      for (int pc = wave; pc * 1024 < nbytes; pc += kWaves)
+      for (int pc = wave; pc * 1024 < nbytes + (STREAM ? kAhead : 0); pc += kWaves)
         dma16(entb + a0 + pc * 1024 + lane * 16, lds + kIdxBase + buf * kIdxBytes + pc * 1024);
     // headers ride the same vmcnt wait: lanes 0..kRW hold chunk k's row starts of
     // this wave's rows, lanes kRW+1 / kRW+2 the block bounds of the chunk after it
@@ -216,6 +229,18 @@ __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
   f4 acc[kRW];
 #pragma unroll
   for (int r = 0; r < kRW; ++r) acc[r] = f4{0.f, 0.f, 0.f, 0.f};
+  // STREAM: the row accumulators as one register tuple (dynamic row index ->
+  // s_set_gpr_idx_on moves; a static index is a plain register)
+  typedef float v32 __attribute__((ext_vector_type(32)));
+  static_assert(kRW * 4 == 32, "the accumulator tuple holds kRW f4 rows");
+  v32 accv = 0.f;
+  auto vget = [&](int r) -> f4 { return f4{accv[4 * r], accv[4 * r + 1], accv[4 * r + 2], accv[4 * r + 3]}; };
+  auto vset = [&](int r, f4 a) {
+    accv[4 * r] = a.x;
+    accv[4 * r + 1] = a.y;
+    accv[4 * r + 2] = a.z;
+    accv[4 * r + 3] = a.w;
+  };
   const uint32_t lane16 = uint32_t(lane) * 16;
   if (threadIdx.x < 128)  // the two stages' zero pieces (pads read them); visible after the first barrier
     *reinterpret_cast<f4*>(lds + (threadIdx.x >> 6) * kStage + kZeroRel + lane16) = f4{0.f, 0.f, 0.f, 0.f};
@@ -231,6 +256,7 @@ __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
       int bnd[kRW + 1];  // header words: (even) first entry | 1 if the row's segment ends in a pad entry
 #pragma unroll
       for (int i = 0; i <= kRW; ++i) bnd[i] = __builtin_amdgcn_readlane(hv, i) & ~1;
+      const int hcur = hv;  // this chunk's header lanes (issue() below loads the next chunk's into hv)
       const int e0 = blk0 & ~1;
       const bool fits = int64_t((blk1 & ~1) - e0) * 8 <= kIdxBytes - kAhead;
       blk0 = __builtin_amdgcn_readlane(hv, kRW + 1);  // the next chunk's block, for the issue below
@@ -242,11 +268,15 @@ __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
       auto gather = [&](int32_t o) { return *reinterpret_cast<const f4*>(lds + piece_addr(uint32_t(o), lb)); };
       if (!fits) {  // an over-full block (denser graphs): indices from global memory, same order
 #pragma unroll
-        for (int r = 0; r < kRW; ++r)
+        for (int r = 0; r < kRW; ++r) {
+          f4 a = STREAM ? vget(r) : acc[r];
           for (int e = bnd[r]; e < bnd[r + 1]; ++e) {
             const int64_t q = int64_t(e >> 1) * 4 + 2 * (e & 1);  // (weight, offset)
-            acc[r] = fmac(acc[r], __int_as_float(ent[q]), gather(ent[q + 1]));
+            a = fmac(a, __int_as_float(ent[q]), gather(ent[q + 1]));
           }
+          if constexpr (STREAM) vset(r, a);
+          else acc[r] = a;
+        }
         continue;
       }
       // This wave's rows' segments are one contiguous run of entry pairs in the
@@ -260,6 +290,55 @@ __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
       // `fits` leaves the room).
       const uint32_t ibase = uint32_t(kIdxBase + (g & 1) * kIdxBytes) - uint32_t(e0) * 8;
       auto pair_at = [&](uint32_t a) { return *static_cast<const I4*>(__builtin_assume_aligned(lds + a, 16)); };
+      if constexpr (STREAM) {
+        const int b0 = bnd[0];
+        const int n = (bnd[kRW] - b0) >> 1;  // the wave's pairs in this chunk (all rows, pads included)
+        if (n == 0) continue;
+        // B(r): pair index where row r starts (B(kRW) = n)
+        auto B = [&](int r) { return ((__builtin_amdgcn_readlane(hcur, r) & ~1) - b0) >> 1; };
+        const uint32_t pa0 = ibase + uint32_t(b0) * 8;  // LDS address of the run's pair 0
+        int r = 0, jb = 0;  // the current row; pair index of this 6-step block's first step
+        int nb = B(1);      // pair index where the next row starts
+        int nbr = nb;       // ... relative to jb
+        uint32_t pb = pa0;  // LDS address of pair jb
+        f4 a = vget(0);
+        I4 I0 = pair_at(pa0), I1 = pair_at(pa0 + 16), I2;
+        f4 G0a = gather(I0.o0), G0b = gather(I0.o1), G1a, G1b;
+        // step K of the block (pair jb + K): at a row boundary move the running
+        // sum (and skip empty rows; the run's end is the last boundary); then
+        // the index two pairs ahead, the gathers one pair ahead, this pair's sum
+#define DOL_SLAB_STEP(K, IC, IN, INN, GCA, GCB, GNA, GNB)                      \
+        if (nbr == K) {                                                          \
+          if (jb + K == n) goto stream_done;                                     \
+          vset(r, a);                                                            \
+          do { /* rows empty in this chunk keep their sums */                    \
+            r = __builtin_amdgcn_readfirstlane(r + 1);                           \
+            nb = B(r + 1);                                                       \
+          } while (nb == jb + K);                                                \
+          a = vget(r);                                                           \
+          nbr = nb - jb;                                                         \
+        }                                                                        \
+        INN = pair_at(pb + 16 * (K + 2));                                        \
+        GNA = gather(IN.o0);                                                     \
+        GNB = gather(IN.o1);                                                     \
+        a = fmac(a, __int_as_float(IC.w0), GCA);                                 \
+        a = fmac(a, __int_as_float(IC.w1), GCB);
+        for (;;) {
+          DOL_SLAB_STEP(0, I0, I1, I2, G0a, G0b, G1a, G1b)
+          DOL_SLAB_STEP(1, I1, I2, I0, G1a, G1b, G0a, G0b)
+          DOL_SLAB_STEP(2, I2, I0, I1, G0a, G0b, G1a, G1b)
+          DOL_SLAB_STEP(3, I0, I1, I2, G1a, G1b, G0a, G0b)
+          DOL_SLAB_STEP(4, I1, I2, I0, G0a, G0b, G1a, G1b)
+          DOL_SLAB_STEP(5, I2, I0, I1, G1a, G1b, G0a, G0b)
+          jb += 6;
+          nbr -= 6;
+          pb += 96;
+        }
+#undef DOL_SLAB_STEP
+      stream_done:
+        vset(r, a);
+        continue;
+      }
       auto step2 = [&](f4 a, const I4& p, const I4& q) {  // four entries: p's pair, then q's
         const f4 x0 = gather(p.o0), x1 = gather(p.o1), x2 = gather(q.o0), x3 = gather(q.o1);
         if constexpr (PROBE == 5) return a + x0 + x1 + x2 + x3;
@@ -326,12 +405,13 @@ __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
 #pragma unroll
       for (int r = 0; r < kRW; ++r) {
         const int row = pr[r];  // this wave's slot r holds output row `row` (-1: none)
+        const f4 v = STREAM ? vget(r) : acc[r];
         if (row >= 0) {
           float* y = Y + int64_t(row) * ldy + p;
           if (p + 4 <= P) {
-            __builtin_nontemporal_store(acc[r], reinterpret_cast<f4*>(y));
+            __builtin_nontemporal_store(v, reinterpret_cast<f4*>(y));
           } else {
-            for (int c = 0; c < int(P - p); ++c) y[c] = acc[r][c];
+            for (int c = 0; c < int(P - p); ++c) y[c] = v[c];
           }
         }
       }
@@ -339,6 +419,7 @@ __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
     if (!has_next) break;
 #pragma unroll
     for (int r = 0; r < kRW; ++r) acc[r] = f4{0.f, 0.f, 0.f, 0.f};
+    accv = 0.f;
     t += G;
     cur = nxt;
     nxt = nn;
@@ -635,7 +716,33 @@ __global__ __launch_bounds__(64) void slab_scatter_kernel(const int32_t* __restr
   }
 }
 
+// kTailPad pad entries (weight 0, the zero piece) right after the last block:
+// the stream kernel reads up to two pairs past a wave's run, and past the last
+// block ent is otherwise unwritten.  hdr[blocks - 1] (the last group's
+// terminator slot, count 0) holds the total after the exclusive scan.
+constexpr int kTailPad = 8;
+__global__ void slab_tail_kernel(const int32_t* __restrict__ hdr, int64_t blocks, int32_t* __restrict__ ent) {
+  const int64_t total = hdr[blocks - 1];
+  const int t = threadIdx.x;
+  if (t < kTailPad) {
+    const int64_t e = total + t;
+    const int64_t q = (e >> 1) * 4 + 2 * (e & 1);
+    ent[q] = 0;
+    ent[q + 1] = kZeroRel;
+  }
+}
+static_assert(kTailPad <= kEntPad, "the tail pads fit the entry slack");
+
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// kernel of dol_mix_csr_slab_f32 (dol_slab_set_variant): 0 = the process
+// default (DOL_SLAB_KERNEL, else the row-loop kernel), 1 = row loop (r03),
+// 2 = pipelined stream (r06).  Atomic: thread-compatible like the other setters.
+std::atomic<int> g_slab_variant{0};
+int slab_default_variant() {
+  static const int v = [] { const char* e = getenv("DOL_SLAB_KERNEL"); return (e && atoi(e) == 2) ? 2 : 1; }();
+  return v;
+}
 
 // segment alignment of the packing and the kernel variant that reads it (one
 // value per process): 2 = pairs; 4 = pairs of pairs, so a row's tail is at most
@@ -646,6 +753,15 @@ int slab_align() {
 }
 
 }  // namespace
+
+extern "C" int dol_slab_set_variant(int32_t variant) {
+  if (variant < 0 || variant > 2)
+    return dol::fail(DOL_EINVAL, "dol_slab_set_variant: variant %d outside 0 (default) / 1 (row loop) / 2 (stream)",
+                     variant);
+  const int prev = g_slab_variant.exchange(variant, std::memory_order_relaxed);
+  dol::g_err[0] = '\0';
+  return prev;
+}
 
 extern "C" int dol_csr_slab_nk(int32_t x_rows) { return x_rows <= 0 ? 0 : int((int64_t(x_rows) + kChunk - 1) / kChunk); }
 extern "C" int64_t dol_csr_slab_hdr_len(int32_t n_rows, int32_t x_rows) {
@@ -703,7 +819,12 @@ extern "C" int dol_mix_csr_slab_f32(const float* X, int64_t ldx, int32_t x_rows,
   else if (probe == 5) launch(csr_slab_kernel<5>);
   else if (probe == 6) launch(csr_slab_kernel<6>);
   else if (slab_align() == 4) launch(csr_slab_kernel<0, true>);
-  else launch(csr_slab_kernel<0>);
+  else {
+    int v = g_slab_variant.load(std::memory_order_relaxed);
+    if (v == 0) v = slab_default_variant();
+    if (v == 2) launch(csr_slab_kernel<0, false, true>);
+    else launch(csr_slab_kernel<0>);
+  }
   return dol::check_launch("dol_mix_csr_slab_f32");
 }
 
@@ -731,6 +852,7 @@ extern "C" int dol_csr_slab_pack(const int32_t* rowptr, const int32_t* col, cons
   hipLaunchKernelGGL(slab_scan_kernel, dim3(1), dim3(1024), 0, s, hdr, blocks);
   hipLaunchKernelGGL(slab_scatter_kernel, dim3(static_cast<unsigned>(n_rows)), dim3(64), 0, s, rowptr, col, val, nk,
                      inv, hdr, ent, slab_align());
+  hipLaunchKernelGGL(slab_tail_kernel, dim3(1), dim3(64), 0, s, hdr, blocks, ent);
   return dol::check_launch("dol_csr_slab_pack");
 }
 

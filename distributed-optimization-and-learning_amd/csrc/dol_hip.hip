@@ -1201,7 +1201,7 @@ __device__ __forceinline__ double block_sum_f64_nt(double v, double* smem) {
   return s;
 }
 
-template <typename V, bool MOM, bool RESID, int NT>
+template <typename V, bool MOM, bool RESID, int NT, int PF = kRoundPF>
 __global__ __launch_bounds__(NT) void admm_ls_round_mean_kernel(
     float* __restrict__ W, int64_t ldw, float* __restrict__ B, int64_t ldb, float* __restrict__ A, int64_t lda,
     const float* __restrict__ T, int64_t ldt, const float* __restrict__ theta, const int32_t* __restrict__ agents,
@@ -1232,12 +1232,12 @@ __global__ __launch_bounds__(NT) void admm_ls_round_mean_kernel(
   V acc = vzero(th);
   double rw = 0.0, ra = 0.0;
   struct Grp {
-    V t[kRoundPF], a[kRoundPF], b[kRoundPF];
-    int64_t row[kRoundPF];
+    V t[PF], a[PF], b[PF];
+    int64_t row[PF];
   };
-  auto load = [&](Grp& g, int k0) {  // agents k0 .. k0 + kRoundPF - 1, unconditionally (rows clamped)
+  auto load = [&](Grp& g, int k0) {  // agents k0 .. k0 + PF - 1, unconditionally (rows clamped)
 #pragma unroll
-    for (int u = 0; u < kRoundPF; ++u) {
+    for (int u = 0; u < PF; ++u) {
       g.row[u] = row_of(k0 + u);
       g.t[u] = ldnt(cptr(T, ldt, g.row[u]));
       g.a[u] = ldnt(cptr(A, lda, g.row[u]));
@@ -1256,18 +1256,18 @@ __global__ __launch_bounds__(NT) void admm_ls_round_mean_kernel(
     ra += live ? rau : 0.0;
     acc = k == 0 ? w : vadd(acc, w);
   };
-  const int ng = (m + kRoundPF - 1) / kRoundPF;  // groups; all but the last are full
+  const int ng = (m + PF - 1) / PF;  // groups; all but the last are full
   Grp nxt, cur;
   load(nxt, 0);
   for (int gi = 0; gi + 1 < ng; ++gi) {  // straight-line body: the same memory ops every trip
     cur = nxt;
-    load(nxt, (gi + 1) * kRoundPF);      // the next group's loads fly during this group's steps
+    load(nxt, (gi + 1) * PF);      // the next group's loads fly during this group's steps
 #pragma unroll
-    for (int u = 0; u < kRoundPF; ++u) run(cur, u, gi * kRoundPF + u);
+    for (int u = 0; u < PF; ++u) run(cur, u, gi * PF + u);
   }
 #pragma unroll
-  for (int u = 0; u < kRoundPF; ++u) {   // the last group (maybe partial)
-    const int k = (ng - 1) * kRoundPF + u;
+  for (int u = 0; u < PF; ++u) {   // the last group (maybe partial)
+    const int k = (ng - 1) * PF + u;
     if (k < m) run(nxt, u, k);
   }
   if (live) {
@@ -2256,7 +2256,7 @@ int dol_admm_ls_round_f32(float* w, int64_t ldw, float* buf, int64_t ldb, float*
 
 int64_t dol_admm_ls_round_mean_workspace_bytes(int64_t P) {
   if (P <= 0 || P > dol::kMaxDim) return 0;
-  return 2 * (cdiv(P, kThreads) + 1) * int64_t(sizeof(double));  // [2][blocks]: (w - theta)^2, alpha^2
+  return 2 * (cdiv(P, 64) + 2) * int64_t(sizeof(double));  // [2][blocks]: (w - theta)^2, alpha^2 (64-lane blocks)
 }
 
 int dol_admm_ls_round_mean_f32(float* w, int64_t ldw, float* buf, int64_t ldb, float* alpha, int64_t lda,
@@ -2285,9 +2285,25 @@ int dol_admm_ls_round_mean_f32(float* w, int64_t ldw, float* buf, int64_t ldb, f
                       row_vec_ok(theta, 0) && row_vec_ok(theta_out, 0) && (!mom || row_vec_ok(buf, ldb));
   const ColSplit cs = split_cols(P, vec_ok);
   // column strip per workgroup: 1024 lanes (16 KiB of each row per workgroup,
-  // one workgroup per CU at 2^20 columns) unless DOL_ADMM_ROUND_THREADS=256
-  static const bool wide = env_int("DOL_ADMM_ROUND_THREADS", 1024) != 256;
-  const int64_t nt = wide ? 1024 : 256;
+  // one workgroup per CU at 2^20 columns) unless DOL_ADMM_ROUND_THREADS=256.
+  // Narrower blocks (fewer than 1024 lanes per CU) take 256-lane strips: the
+  // strips are the only parallelism (the sum over agents is sequential per
+  // column).  At 8192 x 2^17 (a column-sharded rank's block at 8 ranks):
+  // 18.6 ms with 1024-lane strips, 7.4 with 256, 7.65 with one-wave strips
+  // and 8 agents in flight -- and 5.15 for the two-kernel round (row-major
+  // client round + ordered sum), which SeparableADMM(shard="columns") takes
+  // there (profiles/r06c_admm_narrow_ab.jsonl).
+  static const int threads_env = env_int("DOL_ADMM_ROUND_THREADS", 0);
+  static const int n_cu = [] {
+    int dev = 0, cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cu = 256;
+    return cu > 0 ? cu : 256;
+  }();
+  const int64_t lanes = std::max<int64_t>(cs.n4, cs.tail);
+  const int nt = threads_env == 256 || threads_env == 64 || threads_env == 1024 ? threads_env
+                 : (lanes >= int64_t(1024) * n_cu ? 1024 : 256);
+  const bool wide = nt == 1024;
   const int64_t nb4 = cdiv(cs.n4, nt), nbt = cdiv(cs.tail, nt);
   const int64_t nb = nb4 + nbt;
   double* partial = static_cast<double*>(work);
@@ -2295,8 +2311,9 @@ int dol_admm_ls_round_mean_f32(float* w, int64_t ldw, float* buf, int64_t ldb, f
   auto go = [&](auto vt, auto mc, auto rc, int64_t c_off, int64_t ncols, int64_t blocks, int64_t part_off) {
     using V = decltype(vt);
     constexpr bool M = decltype(mc)::value, R = decltype(rc)::value;
-    auto k = wide ? admm_ls_round_mean_kernel<V, M, R, 1024> : admm_ls_round_mean_kernel<V, M, R, 256>;
-    hipLaunchKernelGGL(k, dim3(static_cast<unsigned>(blocks)), dim3(wide ? 1024 : 256), 0, s, w, ldw, buf, ldb, alpha,
+    auto k = wide ? admm_ls_round_mean_kernel<V, M, R, 1024>
+                  : nt == 256 ? admm_ls_round_mean_kernel<V, M, R, 256> : admm_ls_round_mean_kernel<V, M, R, 64, 8>;
+    hipLaunchKernelGGL(k, dim3(static_cast<unsigned>(blocks)), dim3(nt), 0, s, w, ldw, buf, ldb, alpha,
                        lda, target, ldt, theta, agents, first, m, c_off, ncols, rho, -lr, momentum, local_steps,
                        theta_out, scale, do_div, partial, part_off, nb);
   };

@@ -81,6 +81,7 @@ SIGNATURES = {
     "dol_csr_slab_ent_len": [_i64, _i32, _i32],
     "dol_mix_csr_slab_f32": [_ptr, _i64, _i32, _ptr, _i64, _i32, _i64, _ptr, _ptr, _ptr],
     "dol_csr_slab_pack": [_ptr, _ptr, _ptr, _i32, _i32, _i32, _ptr, _ptr, _ptr],
+    "dol_slab_set_variant": [_i32],
     "dol_dense_to_csr_f32": [_ptr, _i64, _i32, _i32, _ptr, _ptr, _ptr, _i64, _ptr],
     "dol_bank_alloc": [_i64, _ptr, _ptr],  # (bytes, void** out, int64_t* out): addresses of host words
     "dol_bank_free": [_ptr, _i64],

@@ -309,6 +309,15 @@ def csr_slab_pack(rowptr: torch.Tensor, col: torch.Tensor, val: torch.Tensor, x_
     return ent, hdr
 
 
+SLAB_VARIANTS = (1, 2)  # 1: a loop per (row, chunk) segment (r03); 2: the wave's pairs as one pipelined stream (r06)
+
+
+def slab_variant(variant: int) -> int:
+    """Kernel of mix_csr_slab for this process (dol_slab_set_variant; 0 =
+    the default).  Same bits for every variant.  Returns the previous setting."""
+    return int(_native.lib().dol_slab_set_variant(int(variant)))
+
+
 def slab_layout_ok(X: torch.Tensor, Y: torch.Tensor, P: int) -> bool:
     """Whether mix_csr_slab accepts these matrices: 16-B aligned rows, row
     strides multiples of 4, X rows readable up to round_up(P, 4) floats."""

@@ -161,10 +161,18 @@ class SeparableADMM:
         # process, or the 'fast' mean's local part; off with injected checkers
         # or DOL_ADMM_FUSED_MEAN=0
         import os
+        auto = fused is None
         if fused is None:
             fused = os.environ.get("DOL_ADMM_FUSED_MEAN", "1") != "0"
         self.fused = bool(fused) and round_fn is None and ordered_sum is None and \
             (self.world == 1 or mean == "fast" or shard == "columns")
+        if auto and self.fused and shard == "columns" and self.world > 1 and self.device.type == "cuda":
+            # the one-pass kernel's parallelism is its column strips: below ~1024 lanes
+            # per CU the two-kernel round (row-major client round, then the ordered
+            # sum) is faster -- 5.15 vs 7.4 ms at 8192 x 2^17, a rank's block at 8
+            # ranks (profiles/r06c_admm_narrow_ab.jsonl); same bits either way
+            n_cu = torch.cuda.get_device_properties(self.device).multi_processor_count
+            self.fused = self.Pl >= 4 * 1024 * n_cu
         self._round_mean = ops.admm_ls_round_mean
         self._parallel = parallel
         self.rs = np.random.RandomState(seed)  # the reference's np.random.choice stream (setup_seed)

@@ -354,7 +354,7 @@ def test_sharded_admm_real_kernels_on_one_gpu(world, mean, gpu):
             np.testing.assert_allclose(r[4], th, rtol=1e-5, atol=1e-6)
 
 
-def _admm_col_worker(rank, world, port, N, P, rounds, kw, q):
+def _admm_col_worker(rank, world, port, N, P, rounds, kw, q, fused=None):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, os.path.join(root, "distributed-optimization-and-learning_amd"))
@@ -364,8 +364,9 @@ def _admm_col_worker(rank, world, port, N, P, rounds, kw, q):
     os.environ["MASTER_PORT"] = str(port)
     parallel.init_process_group("gloo", rank=rank, world_size=world, timeout_s=120)
     try:
-        s = SeparableADMM(N, P, device=torch.device("cuda:0"), shard="columns", **kw)
-        assert s.fused  # the one-pass kernel over this rank's columns
+        s = SeparableADMM(N, P, device=torch.device("cuda:0"), shard="columns", fused=fused, **kw)
+        # narrow blocks take the two-kernel round by default; fused=True forces the one-pass kernel
+        assert s.fused == (fused is True)
         for _ in range(rounds):
             s.round()
         torch.cuda.synchronize()
@@ -376,10 +377,11 @@ def _admm_col_worker(rank, world, port, N, P, rounds, kw, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [3, 8])
-def test_column_sharded_admm_real_kernels_on_one_gpu(world, gpu):
-    """SeparableADMM(shard="columns") with the real one-pass kernel
-    (dol_admm_ls_round_mean_f32 over each rank's parameter columns, all
+@pytest.mark.parametrize("world,fused", [(3, None), (8, None), (3, True), (8, True)])
+def test_column_sharded_admm_real_kernels_on_one_gpu(world, fused, gpu):
+    """SeparableADMM(shard="columns") with the real kernels (the one-pass
+    dol_admm_ls_round_mean_f32 when forced, else -- narrow blocks -- the
+    two-kernel round + ordered sum; each over the rank's parameter columns, all
     sampled agents in the global order): rows, duals, momentum and theta
     bit-identical to one process; no collective on the round path (VERDICT r05
     item 6; DEC/servers.py:42-48,50-81)."""
@@ -393,7 +395,8 @@ def test_column_sharded_admm_real_kernels_on_one_gpu(world, gpu):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_admm_col_worker, args=(r, world, port, N, P, rounds, kw, q)) for r in range(world)]
+    procs = [ctx.Process(target=_admm_col_worker, args=(r, world, port, N, P, rounds, kw, q, fused))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda t: t[0])

@@ -45,6 +45,14 @@ def special_x(n, P, seed):
     return X
 
 
+@pytest.fixture(params=ops.SLAB_VARIANTS)
+def slab_variant(request):
+    """Every slab test runs under each kernel variant (dol_slab_set_variant)."""
+    prev = ops.slab_variant(request.param)
+    yield request.param
+    ops.slab_variant(prev)
+
+
 def bank_like(X, gpu, ld):
     n, P = X.shape
     t = torch.full((n, ld), float("nan"), dtype=torch.float32, device=gpu)
@@ -60,7 +68,7 @@ def bank_like(X, gpu, ld):
     (512, 700, 0.9, 0),      # over-full index blocks: the global-memory index path
     (100, 1024, 1.0, 0),     # the complete graph
 ])
-def test_slab_mix_matches_oracle(n, P, p, ld_extra, gpu):
+def test_slab_mix_matches_oracle(n, P, p, ld_extra, gpu, slab_variant):
     csr = er_csr(n, p, seed=n + P, empty_rows=(1, n - 1))
     plan = G.MixingPlan(csr, gpu, slab=True)
     assert plan.kind == "csr" and plan.ent is not None
@@ -79,7 +87,7 @@ def test_slab_mix_matches_oracle(n, P, p, ld_extra, gpu):
     assert torch.isnan(Yd[:, P:]).all(), "wrote past P"
 
 
-def test_slab_rectangular_and_low_degree_rows(gpu):
+def test_slab_rectangular_and_low_degree_rows(gpu, slab_variant):
     """More X rows than Y rows (a column block of agents), rows of degree 0, 1
     and every column, neighbours confined to one chunk or spread over all."""
     n, m, P = 40, 200, 512
@@ -191,10 +199,13 @@ def test_slab_pack_matches_host(n, p, balance, gpu):
     pairs = ent_d[: 2 * len(ent)].cpu().numpy().reshape(-1, 4)  # (w0, off0, w1, off1)
     got_e = np.stack([pairs[:, [1, 3]].reshape(-1), pairs[:, [0, 2]].reshape(-1)], axis=1)
     assert np.array_equal(got_e, ent)
+    # r06: pad entries right after the last block (the stream kernel reads up to two pairs past a run)
+    tail = ent_d[2 * len(ent): 2 * len(ent) + 16].cpu().numpy().reshape(-1, 2)
+    assert np.array_equal(tail, np.tile([0, SLAB_ZERO_OFFSET], (8, 1)))
 
 
 @pytest.mark.parametrize("n,P,p", [(1024, 2560, 0.1), (300, 1001, 0.3)])
-def test_slab_balanced_pack_mixes_bit_exactly(n, P, p, gpu):
+def test_slab_balanced_pack_mixes_bit_exactly(n, P, p, gpu, slab_variant):
     """Rows dealt to waves by the greedy packing: the same sums in the same
     order, so the same bits as the row-order packing and the oracle."""
     csr = er_csr(n, p, seed=n + 7, empty_rows=(2,))
@@ -267,7 +278,7 @@ def test_from_dense_csr_plan_reuse_and_mix(gpu):
         assert bits_equal(Yd[:, :P].cpu().numpy(), oracle.mix_csr(X, host.rowptr, host.col, host.val))
 
 
-def test_slab_full_size_config5(gpu):
+def test_slab_full_size_config5(gpu, slab_variant):
     """1024 agents x 101,770 (config 5's MLP), ER p = 0.1: bit-identical to the
     generic CSR kernel everywhere and to the oracle on sampled rows."""
     from dolhip.bank import row_stride
@@ -292,7 +303,7 @@ def test_slab_full_size_config5(gpu):
     assert bits_equal(Yd[rows][:, cols].cpu().numpy(), oracle.mix_csr(Xs, sub.rowptr, sub.col, sub.val))
 
 
-def test_slab_8192_agents(gpu):
+def test_slab_8192_agents(gpu, slab_variant):
     n, P = 8192, 1024
     W = G.erdos_renyi_stochastic_hip(n, 0.1, seed=11, device=gpu)
     plan = G.MixingPlan.from_dense(W, dense_kernel="csr")
