@@ -137,11 +137,32 @@ struct DgdEpi {
   float* __restrict__ M; int64_t ldm;
   float neg_lr, mom;
   int steps;
+  // Target / momentum rows are read once: buffer loads with the nontemporal
+  // policy (aux 3 = sc0 nt), so they do not push the X halo rows -- re-read by
+  // the next row group's tile, 1024 workgroups later -- out of the XCD's L2.
+  // With plain loads the ring round read 1.16x its bytes (14.97 vs 12.88 GB
+  // at 1024 x 2^20, least squares + momentum) and ran 3.58-3.59 ms; with these
+  // 12.90 GB = 1.00x and 3.44-3.45 ms (profiles/r06f_dgd_epi_policy.jsonl; sc0
+  // sc1 without nt: no change).  DOL_DGD_EPI_NT=0 restores plain loads, 1 the
+  // compiler's nontemporal global loads.
+  int nt;
 
+  template <typename V> __device__ __forceinline__ V ld(const float* row, int64_t cf) const {
+    const V* p = reinterpret_cast<const V*>(row + cf);
+    if constexpr (sizeof(V) == 16) {
+      if (nt == 3) {
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(row), 0, 0x7ffffff0, 0x00020000);
+        return __builtin_bit_cast(V, __builtin_amdgcn_raw_buffer_load_b128(rs, uint32_t(cf) * 4u, 0, 3));
+      }
+      if (nt == 1) return __builtin_nontemporal_load(p);
+    }
+    return *p;
+  }
   template <typename V> __device__ __forceinline__ DgdState<V> load(int r, int64_t cf) const {
     DgdState<V> st;
-    st.t = *reinterpret_cast<const V*>(T + int64_t(r) * ldt + cf);
-    if constexpr (MODE == 2) st.b = *reinterpret_cast<const V*>(M + int64_t(r) * ldm + cf);
+    st.t = ld<V>(T + int64_t(r) * ldt, cf);
+    if constexpr (MODE == 2) st.b = ld<V>(M + int64_t(r) * ldm, cf);
     else st.b = vzero(V{});
     return st;
   }
@@ -1831,9 +1852,12 @@ int check_dgd(const char* nm, const DgdArgs& d, int64_t P, bool* evec, int* mode
 }
 
 template <class F>
-int with_dgd_epi(const DgdArgs& d, int mode, F&& f) {
+int with_dgd_epi(const DgdArgs& d, int mode, int64_t P, F&& f) {
+  static const int nt_env = env_int("DOL_DGD_EPI_NT", 3);
+  // buffer offsets are 32-bit (rows of < 2^29 floats); longer rows: plain loads
+  const int nt = (nt_env == 3 && P > (int64_t(1) << 29) - 16) ? 0 : nt_env;
   auto mk = [&](auto obj, auto md) {
-    return f(DgdEpi<decltype(obj)::value, decltype(md)::value>{d.T, d.ldt, d.M, d.ldm, -d.lr, d.momentum, d.steps});
+    return f(DgdEpi<decltype(obj)::value, decltype(md)::value>{d.T, d.ldt, d.M, d.ldm, -d.lr, d.momentum, d.steps, nt});
   };
   using std::integral_constant;
   if (d.objective == 0) {
@@ -1862,7 +1886,7 @@ int dol_dgd_ring_f32(const float* X, int64_t ldx, float* Y, int64_t ldy, int32_t
     const int rc = check_dgd(nm, d, P, &evec, &mode);
     if (rc) return rc;
   }
-  return with_dgd_epi(d, mode, [&](auto epi) {
+  return with_dgd_epi(d, mode, P, [&](auto epi) {
     return mix_ring_impl(nm, X, ldx, Y, ldy, n_rows, P, halo_prev, halo_next, w_prev, w_next, epi, evec, s);
   });
 }
@@ -1880,7 +1904,7 @@ int dol_dgd_ring_edges_f32(const float* X, int64_t ldx, float* Y, int64_t ldy, i
     const int rc = check_dgd(nm, d, P, &evec, &mode);
     if (rc) return rc;
   }
-  return with_dgd_epi(d, mode, [&](auto epi) {
+  return with_dgd_epi(d, mode, P, [&](auto epi) {
     return ring_edges_impl(nm, X, ldx, Y, ldy, n_rows, P, halo_prev, halo_next, w_prev, w_next, epi, evec, s);
   });
 }
@@ -1898,7 +1922,7 @@ int dol_dgd_csr_f32(const float* X, int64_t ldx, int32_t x_rows, float* Y, int64
     const int rc = check_dgd(nm, d, P, &evec, &mode);
     if (rc) return rc;
   }
-  return with_dgd_epi(d, mode, [&](auto epi) {
+  return with_dgd_epi(d, mode, P, [&](auto epi) {
     return mix_csr_impl(nm, X, ldx, x_rows, Y, ldy, n_rows, P, rowptr, col, val, epi, evec, s);
   });
 }
