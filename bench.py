@@ -907,14 +907,13 @@ def main():
     dolhip.lib()
     N, P = args.agents, args.params
     wp, wn = ring_weights(N)
-    # --map-ring 1 (default): at world 1 the headline's two buffers are mapped
-    # physical blocks, like every bank matrix of >= 1 GiB (bank.device_matrix;
-    # in one process 10.69 vs 10.90 ms for torch-allocated ones,
-    # profiles/r05d_alloc_ab.jsonl).  Across ranks the halo rows are RCCL
-    # send/recv buffers: those stay on torch's allocator, the memory every
-    # PyTorch RCCL user hands it (no multi-GPU node here to validate RCCL on
-    # mapped blocks)
-    ring = ShardedRing(N, P, wp, wn, device, mapped=bool(args.map_ring) and world == 1)
+    # --map-ring 1 (default): the headline's two buffers are mapped physical
+    # blocks, like every bank matrix of >= 1 GiB (bank.device_matrix; in one
+    # process 10.69 vs 10.90 ms for torch-allocated ones,
+    # profiles/r05d_alloc_ab.jsonl), at every world size (r06): across ranks the
+    # two boundary rows are copied into torch-allocated send buffers before the
+    # RCCL send (ShardedRing.stage_sends), so every N runs on the same memory
+    ring = ShardedRing(N, P, wp, wn, device, mapped=bool(args.map_ring))
     g = torch.Generator(device=device).manual_seed(2028 + rank)
     ring.x.normal_(generator=g)
     ring.y.zero_()

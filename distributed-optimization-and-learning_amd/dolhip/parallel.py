@@ -107,7 +107,7 @@ class ShardedRing:
 
     def __init__(self, n_agents: int, P: int, w_prev, w_next, device, ld: Optional[int] = None,
                  group=None, alloc: bool = True, mix_ring=None, dgd_ring=None, mix_edges=None, dgd_edges=None,
-                 mapped: Optional[bool] = None):
+                 mapped: Optional[bool] = None, stage_sends: Optional[bool] = None):
         # mix_ring / dgd_ring / *_edges: kernel entries (default: the HIP ops); tests
         # inject CPU checkers.  The boundary rows go in ONE launch (dol_*_ring_edges_f32);
         # with an injected mix and no injected edge entry they go through the mix, one row each.
@@ -131,15 +131,19 @@ class ShardedRing:
         self.w_next = wn[self.lo:self.hi].contiguous().to(self.device)
         self.prev_rank = (self.rank - 1) % self.world
         self.next_rank = (self.rank + 1) % self.world
-        if mapped is None and self.world > 1:
-            # the boundary rows are handed to RCCL send/recv as they are: across
-            # ranks keep them on torch's allocator (the memory RCCL users pass)
-            mapped = False
         if alloc:
+            # x / y as bank matrices (mapped blocks of >= 1 GiB by default, the same
+            # memory as at world 1); across ranks the two boundary rows are copied
+            # into torch-allocated send buffers first (stage_sends), so RCCL only
+            # ever sees the memory PyTorch RCCL users hand it
             self.x = device_matrix(self.n_local, self.ld, self.device, mapped=mapped)
             self.y = device_matrix(self.n_local, self.ld, self.device, mapped=mapped)
         self.halo_prev = torch.empty(self.ld, dtype=torch.float32, device=self.device)
         self.halo_next = torch.empty(self.ld, dtype=torch.float32, device=self.device)
+        if stage_sends is None:
+            stage_sends = self.world > 1 and self.device.type == "cuda"
+        self.stage_sends = bool(stage_sends)
+        self._send = torch.empty(2, self.ld, dtype=torch.float32, device=self.device) if self.stage_sends else None
         # optional (start, end) timing events recorded around the interior kernel
         self.kernel_events = None
 
@@ -156,6 +160,10 @@ class ShardedRing:
         P = self.P
         first, last = x[0, :P], x[self.n_local - 1, :P]
         hp, hn = self.halo_prev[:P], self.halo_next[:P]
+        if self.stage_sends:  # the boundary rows leave from torch-allocated buffers (x may be a mapped block)
+            self._send[0, :P].copy_(first)
+            self._send[1, :P].copy_(last)
+            first, last = self._send[0, :P], self._send[1, :P]
         if self._staged():
             first, last = first.cpu(), last.cpu()  # staged
             self._host_halo = (torch.empty(P), torch.empty(P))  # staged

@@ -528,7 +528,8 @@ def _exercise_parallel(world, rank):
     for edges in (True, False):
         ring = parallel.ShardedRing(N, P, wp, wn, "cpu", ld=P + 2, mix_ring=cpu_mix_ring, dgd_ring=cpu_dgd_ring,
                                     mix_edges=cpu_mix_ring_edges if edges else None,
-                                    dgd_edges=cpu_dgd_ring_edges if edges else None)
+                                    dgd_edges=cpu_dgd_ring_edges if edges else None,
+                                    stage_sends=True if edges else None)  # True: the GPU default at world > 1
         ring.x[:, :P] = torch.from_numpy(X[ring.lo:ring.hi])
         ring.kernel_events = (_FakeEvent(), _FakeEvent())
         ring.step()
