@@ -79,6 +79,8 @@ struct MlpArgs {
   float neg_lr, mom, rho;
   int mode;                      // 0 plain SGD, 1 momentum first step, 2 momentum
   int update;                    // 0: gradients only (forward_backward)
+  int f1_keep;                   // F1 stages W1 / X with the default cache policy (DOL_MLP_F1_KEEP, default 1)
+  int dw1_reverse;               // dW1 walks the agents last to first (DOL_MLP_DW1_REVERSE, default 1)
 #ifdef DOL_MLP_TRACE
   long long* trace;              // tools/mlp_phase.hip: per-agent phase timestamps
 #endif
@@ -462,8 +464,12 @@ __device__ __forceinline__ void mlp_fwd_body(MlpArgs a, float* __restrict__ ws) 
       k = k < d ? k : 0;  // clamped in-bounds; zeroed after landing
       const float* src = (r < h) ? top + oW1 + int64_t(r) * d + k
                                  : xa + int64_t(min(r - h, B - 1)) * a.ldxb + k;
-      // nontemporal (r05: fused step 0.489-0.491 vs 0.496-0.499 ms, profiles/r05zzf_mlp_load_policy_ab.jsonl)
-      __builtin_amdgcn_global_load_lds(DOL_GPTR(src), DOL_LPTR(st + ins * 256), 16, 0, 2);
+      // default policy with dW1 reversed (r06, see dol_mlp_step_f32); nontemporal with
+      // dW1 in agent order (r05: 0.489-0.491 vs 0.496-0.499 ms, profiles/r05zzf_mlp_load_policy_ab.jsonl)
+      if (a.f1_keep)
+        __builtin_amdgcn_global_load_lds(DOL_GPTR(src), DOL_LPTR(st + ins * 256), 16, 0, 0);
+      else
+        __builtin_amdgcn_global_load_lds(DOL_GPTR(src), DOL_LPTR(st + ins * 256), 16, 0, 2);
     }
   };
   // PH 3: W1[32 wave + li][32 kc + 16 hh + 4 j + q] = wres[kc][j][q] (the last KL chunks: park)
@@ -843,7 +849,9 @@ __device__ __forceinline__ void mlp_dw1_body(MlpArgs a, const float* __restrict_
   if constexpr (XG) {
     const uint32_t b = blockIdx.x, l = b >> 3;
     dt = static_cast<int>(l % uint32_t(ndt));
-    agent = static_cast<int>((l / uint32_t(ndt)) * 8 + (b & 7));
+    uint32_t lg = l / uint32_t(ndt);
+    if (a.dw1_reverse) lg = uint32_t((n_agents + 7) / 8) - 1 - lg;  // last agents first, each on its forward's XCD
+    agent = static_cast<int>(lg * 8 + (b & 7));
     if (agent >= n_agents) return;
   } else {
     dt = static_cast<int>(blockIdx.x % ndt);
@@ -977,6 +985,17 @@ extern "C" int dol_mlp_step_f32(float* w, int64_t ldw, float* grad, int64_t ldg,
   if (!update && !grad) return fail(DOL_EINVAL, "dol_mlp_step_f32: update=0 needs a grad buffer to write");
   MlpArgs a{w, ldw, grad, ldg, mom, ldm, theta, alpha, lda, X, ldx_agent, ldx_row, labels, ldy_agent, loss,
             B, d, h, c, -lr, momentum, rho, update ? mode : 0, update ? 1 : 0};
+  // r06: the forward walks the agents first to last and, with dW1 walking them
+  // last to first, every launch starts on the rows the launch before it wrote
+  // last -- still in L2 / the Infinity Cache when F1 stages them with the
+  // default policy (the r05 nontemporal staging gave that up).  Config-5 round
+  // (fused step + exact mix, 1024 agents): 1.378 vs 1.400 ms, the local step
+  // 0.457-0.462 vs 0.477-0.479 ms, three alternating trials; the step alone
+  // 0.475-0.480 vs 0.490-0.494 (profiles/r06m_mlp_order.jsonl).  Same bits.
+  static const int f1_keep = [] { const char* e = getenv("DOL_MLP_F1_KEEP"); return e ? atoi(e) : 1; }();
+  static const int dw1_rev = [] { const char* e = getenv("DOL_MLP_DW1_REVERSE"); return e ? atoi(e) : 1; }();
+  a.f1_keep = f1_keep;
+  a.dw1_reverse = dw1_rev;
   const size_t lds = static_cast<size_t>(dol_mlp_step_lds_bytes(B, h, c));
   if (lds > 160 * 1024) return fail(DOL_EINVAL, "dol_mlp_step_f32: %zu B of LDS per agent exceeds 160 KiB", lds);
   const dim3 grid(static_cast<unsigned>(n_agents)), block(kThreads);
