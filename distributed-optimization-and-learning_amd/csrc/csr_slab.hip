@@ -49,6 +49,7 @@
 
 #include "../../include/dol_hip.h"
 #include "dol_common.h"
+#include "csr_slab_stream.inc"
 
 namespace {
 
@@ -70,7 +71,9 @@ constexpr int kZeroRel = kXBytes;
 constexpr int kIdxBytes = 15 * 1024;          // index block capacity per chunk (1920 entries)
 constexpr int kIdxBase = 2 * kStage;
 constexpr int kLds = 2 * kStage + 2 * kIdxBytes;
-constexpr int kAhead = 32;                    // index bytes a wave reads past its stream (two pairs)
+// index bytes a stream variant reads past a wave's run (variant 2: two pairs;
+// variant 3: DOL_SLAB_STREAM_AHEAD pairs)
+constexpr int kAhead = 16 * (DOL_SLAB_STREAM_AHEAD > 2 ? DOL_SLAB_STREAM_AHEAD : 2);
 constexpr int kRW = 8;                        // rows per wave
 constexpr int kRows = kWaves * kRW;           // rows per row group
 constexpr int kEntPad = 160;                  // ent pad entries (the block DMA may read 1 KiB + 8 B past a block)
@@ -148,7 +151,7 @@ __device__ __forceinline__ uint32_t piece_addr(uint32_t o, uint32_t lb) { return
 // per 6.4-entry segment).  Same entries, same order, same bits.  Reads run at
 // most two pairs past the wave's run (kAhead): the index DMA covers them and
 // the packer pads past the last block (slab_tail_kernel).
-template <int PROBE = 0, bool A4 = false, bool STREAM = false>
+template <int PROBE = 0, bool A4 = false, int SV = 0>
 __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
     const float* __restrict__ X, int64_t ldx, int x_rows, float* __restrict__ Y, int64_t ldy, int n_rows, int64_t P,
     const int32_t* __restrict__ ent, const int32_t* __restrict__ hdr, int nk, int n_rg, int64_t n_slabs,
@@ -158,8 +161,13 @@ __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
   const int64_t p4 = (P + 3) / 4 * 4;  // X rows are readable up to here (dol_hip.h)
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // SA (the asm stream, SV 2): DMA addresses as a uniform row base plus this
+  // lane's 32-bit column byte offset (the host keeps round_up(P, 4) * 4 < 2^32),
+  // so an item is uniform state only -- the stream's registers come from here
+  constexpr bool SA = SV == 2;
   struct Item {
     int rg;
+    int64_t slab;            // uniform
     int64_t p;               // this lane's first column
     const float* xsrc;       // X + the in-bounds DMA column of this lane
     const int32_t* H;        // the row group's chunk blocks
@@ -170,11 +178,19 @@ __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
     const int64_t slab = int64_t(local / uint32_t(n_rg)) * 8 + (t & 7);
     if (slab >= n_slabs) return false;
     it.rg = int(local % uint32_t(n_rg));
-    it.p = slab * kCols + lane * 4;
-    const int64_t pl = it.p + 4 <= p4 ? it.p : p4 - 4;  // lanes past P: values unused, reads kept inside round_up(P, 4)
-    it.xsrc = X + pl;
+    it.slab = slab;
+    if constexpr (!SA) {
+      it.p = slab * kCols + lane * 4;
+      const int64_t pl = it.p + 4 <= p4 ? it.p : p4 - 4;  // lanes past P: values unused, reads kept inside round_up(P, 4)
+      it.xsrc = X + pl;
+    }
     it.H = hdr + int64_t(it.rg) * nk * (kRows + 1);
     return true;
+  };
+  // SA: this lane's in-bounds DMA column of slab `slab`, in bytes
+  auto col_bytes = [&](int64_t slab) -> uint32_t {
+    const int64_t p = slab * kCols + lane * 4;
+    return uint32_t((p + 4 <= p4 ? p : p4 - 4) * 4);
   };
   const int32_t* perm = hdr + int64_t(n_rg) * nk * (kRows + 1);  // slot -> output row (dol_csr_slab_pack)
   int64_t t = blockIdx.x;
@@ -198,7 +214,14 @@ __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
       // again, never referenced)
       const int a0w = k * kChunk + wave * kPerWave;
       const uint32_t la = lds_base + uint32_t(buf * kStage + wave * kPerWave * 1024);
-      if (a0w + kPerWave <= x_rows) {
+      if constexpr (SA) {
+        const uint32_t cb = col_bytes(it.slab);
+#pragma unroll
+        for (int i = 0; i < kPerWave; ++i) {
+          const float* row = X + int64_t(min(a0w + i, x_rows - 1)) * ldx;  // uniform
+          asm volatile("global_load_lds_dwordx4 %0, %1" ::"v"(cb), "s"(row), "{m0}"(la + i * 1024) : "memory");
+        }
+      } else if (a0w + kPerWave <= x_rows) {
         const float* src = it.xsrc + int64_t(a0w) * ldx;
 #pragma unroll
         for (int i = 0; i < kPerWave; ++i)
@@ -215,8 +238,15 @@ __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
     const int64_t a0 = int64_t(blk0 & ~1) * 8;  // even: 16-B aligned
     const int64_t nbytes = int64_t(blk1 & ~1) * 8 - a0;
     if (nbytes <= kIdxBytes - kAhead)
-      for (int pc = wave; pc * 1024 < nbytes + (STREAM ? kAhead : 0); pc += kWaves)
-        dma16(entb + a0 + pc * 1024 + lane * 16, lds + kIdxBase + buf * kIdxBytes + pc * 1024);
+      for (int pc = wave; pc * 1024 < nbytes + (SV ? kAhead : 0); pc += kWaves) {
+        if constexpr (SA) {
+          const uint32_t la = lds_base + uint32_t(kIdxBase + buf * kIdxBytes + pc * 1024);
+          asm volatile("global_load_lds_dwordx4 %0, %1" ::"v"(uint32_t(lane) * 16), "s"(entb + a0 + pc * 1024), "{m0}"(la)
+                       : "memory");
+        } else {
+          dma16(entb + a0 + pc * 1024 + lane * 16, lds + kIdxBase + buf * kIdxBytes + pc * 1024);
+        }
+      }
     // headers ride the same vmcnt wait: lanes 0..kRW hold chunk k's row starts of
     // this wave's rows, lanes kRW+1 / kRW+2 the block bounds of the chunk after it
     const int32_t* hb = it.H + int64_t(k + 1) * (kRows + 1);   // (it, k + 1)
@@ -269,15 +299,15 @@ __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
       if (!fits) {  // an over-full block (denser graphs): indices from global memory, same order
 #pragma unroll
         for (int r = 0; r < kRW; ++r) {
-          f4 a = STREAM ? vget(r) : acc[r];
+          f4 a = SV ? vget(r) : acc[r];
           for (int e = bnd[r]; e < bnd[r + 1]; ++e) {
             const int64_t q = int64_t(e >> 1) * 4 + 2 * (e & 1);  // (weight, offset)
             a = fmac(a, __int_as_float(ent[q]), gather(ent[q + 1]));
           }
-          if constexpr (STREAM) vset(r, a);
+          if constexpr (SV != 0) vset(r, a);
           else acc[r] = a;
         }
-        continue;
+        if constexpr (SV != 2) continue;  // SV 2: on into the stream with no pairs (one exit for the tuple)
       }
       // This wave's rows' segments are one contiguous run of entry pairs in the
       // block (row order; every segment an even number of entries, pads
@@ -290,7 +320,18 @@ __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
       // `fits` leaves the room).
       const uint32_t ibase = uint32_t(kIdxBase + (g & 1) * kIdxBytes) - uint32_t(e0) * 8;
       auto pair_at = [&](uint32_t a) { return *static_cast<const I4*>(__builtin_assume_aligned(lds + a, 16)); };
-      if constexpr (STREAM) {
+      if constexpr (SV == 2) {  // variant 3: the same stream, hand-scheduled (csr_slab_stream.inc)
+        const int b0 = bnd[0];
+        const int n = fits ? (bnd[kRW] - b0) >> 1 : 0;  // the stream returns at once on n == 0
+        uint32_t pbv = ibase + uint32_t(b0) * 8;  // LDS address of the run's pair 0 (advanced by the loop)
+        int hb = hcur;  // the header lanes, turned into row-start pair indices by the stream
+        asm volatile(DOL_SLAB_STREAM_ASM
+                     : [acc] DOL_SLAB_STREAM_ACC(accv), [pb] "+v"(pbv), [hc] "+v"(hb)
+                     : [lb] "v"(lb), [n] "s"(n), [b0] "s"(b0)
+                     : DOL_SLAB_STREAM_CLOBBERS, "scc", "memory");
+        continue;
+      }
+      if constexpr (SV == 1) {
         const int b0 = bnd[0];
         const int n = (bnd[kRW] - b0) >> 1;  // the wave's pairs in this chunk (all rows, pads included)
         if (n == 0) continue;
@@ -399,13 +440,13 @@ __global__ __launch_bounds__(kThreads) void csr_slab_kernel(
         acc[r] = a;
       }
     }
-    const int64_t p = cur.p;
+    const int64_t p = SA ? cur.slab * kCols + lane * 4 : cur.p;
     if (p < P) {
       const int32_t* pr = perm + int64_t(cur.rg) * kRows + row0;
 #pragma unroll
       for (int r = 0; r < kRW; ++r) {
         const int row = pr[r];  // this wave's slot r holds output row `row` (-1: none)
-        const f4 v = STREAM ? vget(r) : acc[r];
+        const f4 v = SV ? vget(r) : acc[r];
         if (row >= 0) {
           float* y = Y + int64_t(row) * ldy + p;
           if (p + 4 <= P) {
@@ -737,10 +778,16 @@ inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // kernel of dol_mix_csr_slab_f32 (dol_slab_set_variant): 0 = the process
 // default (DOL_SLAB_KERNEL, else the row-loop kernel), 1 = row loop (r03),
-// 2 = pipelined stream (r06).  Atomic: thread-compatible like the other setters.
+// 2 = pipelined stream (r06), 3 = the stream hand-scheduled (asm; rows of
+// 2^30 floats and more run variant 2).  Atomic: thread-compatible like the
+// other setters.
 std::atomic<int> g_slab_variant{0};
 int slab_default_variant() {
-  static const int v = [] { const char* e = getenv("DOL_SLAB_KERNEL"); return (e && atoi(e) == 2) ? 2 : 1; }();
+  static const int v = [] {
+    const char* e = getenv("DOL_SLAB_KERNEL");
+    const int x = e ? atoi(e) : 1;
+    return (x == 2 || x == 3) ? x : 1;
+  }();
   return v;
 }
 
@@ -755,8 +802,9 @@ int slab_align() {
 }  // namespace
 
 extern "C" int dol_slab_set_variant(int32_t variant) {
-  if (variant < 0 || variant > 2)
-    return dol::fail(DOL_EINVAL, "dol_slab_set_variant: variant %d outside 0 (default) / 1 (row loop) / 2 (stream)",
+  if (variant < 0 || variant > 3)
+    return dol::fail(DOL_EINVAL,
+                     "dol_slab_set_variant: variant %d outside 0 (default) / 1 (row loop) / 2 (stream) / 3 (stream, asm)",
                      variant);
   const int prev = g_slab_variant.exchange(variant, std::memory_order_relaxed);
   dol::g_err[0] = '\0';
@@ -822,7 +870,9 @@ extern "C" int dol_mix_csr_slab_f32(const float* X, int64_t ldx, int32_t x_rows,
   else {
     int v = g_slab_variant.load(std::memory_order_relaxed);
     if (v == 0) v = slab_default_variant();
-    if (v == 2) launch(csr_slab_kernel<0, false, true>);
+    if (v == 2) launch(csr_slab_kernel<0, false, 1>);
+    else if (v == 3 && p4 * 4 < (int64_t(1) << 32)) launch(csr_slab_kernel<0, false, 2>);  // 32-bit column offsets
+    else if (v == 3) launch(csr_slab_kernel<0, false, 1>);
     else launch(csr_slab_kernel<0>);
   }
   return dol::check_launch("dol_mix_csr_slab_f32");

@@ -309,7 +309,7 @@ def csr_slab_pack(rowptr: torch.Tensor, col: torch.Tensor, val: torch.Tensor, x_
     return ent, hdr
 
 
-SLAB_VARIANTS = (1, 2)  # 1: a loop per (row, chunk) segment (r03); 2: the wave's pairs as one pipelined stream (r06)
+SLAB_VARIANTS = (1, 2, 3)  # 1: a loop per (row, chunk) segment (r03); 2: the wave's pairs as one pipelined stream (r06); 3: that stream hand-scheduled (asm)
 
 
 def slab_variant(variant: int) -> int:
