@@ -777,7 +777,7 @@ static_assert(kTailPad <= kEntPad, "the tail pads fit the entry slack");
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // kernel of dol_mix_csr_slab_f32 (dol_slab_set_variant): 0 = the process
-// default (DOL_SLAB_KERNEL, else the row-loop kernel), 1 = row loop (r03),
+// default (DOL_SLAB_KERNEL, else the asm stream), 1 = row loop (r03),
 // 2 = pipelined stream (r06), 3 = the stream hand-scheduled (asm; rows of
 // 2^30 floats and more run variant 2).  Atomic: thread-compatible like the
 // other setters.
@@ -785,8 +785,8 @@ std::atomic<int> g_slab_variant{0};
 int slab_default_variant() {
   static const int v = [] {
     const char* e = getenv("DOL_SLAB_KERNEL");
-    const int x = e ? atoi(e) : 1;
-    return (x == 2 || x == 3) ? x : 1;
+    const int x = e ? atoi(e) : 3;
+    return (x == 1 || x == 2) ? x : 3;
   }();
   return v;
 }

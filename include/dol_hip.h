@@ -150,7 +150,7 @@ int dol_mix_csr_slab_f32(const float* X, int64_t ldx, int32_t x_rows, float* Y, 
 int dol_csr_slab_pack(const int32_t* rowptr, const int32_t* col, const float* val, int32_t n_rows,
                       int32_t x_rows, int32_t balance, int32_t* ent, int32_t* hdr, hipStream_t s);
 /* Kernel of dol_mix_csr_slab_f32 for this process: 0 = default (DOL_SLAB_KERNEL,
- * else 1), 1 = a loop per (row, chunk) segment (r03), 2 = each wave's pairs as
+ * else 3), 1 = a loop per (row, chunk) segment (r03), 2 = each wave's pairs as
  * one software-pipelined stream (r06), 3 = that stream hand-scheduled in
  * assembly (r06; P >= 2^30 runs 2).  Same bits for every variant.  Returns the
  * previous setting, or DOL_EINVAL outside [0, 3].  No reference counterpart (a
