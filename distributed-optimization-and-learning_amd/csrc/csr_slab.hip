@@ -655,19 +655,32 @@ __global__ __launch_bounds__(64) void slab_balance_kernel(int32_t* __restrict__ 
     return;
   }
   int32_t* H = hdr + int64_t(g) * nk * (kRows + 1);
-  for (int64_t j = lane; j < int64_t(kRows) * nk; j += 64) {
-    const int i = int(j / nk), k = int(j % nk);
-    c[j] = uint8_t(H[int64_t(k) * (kRows + 1) + i]);
+  // counts of rows lane and lane + 64, eight chunks' loads in flight at a time
+  // (one dependent global load per element cost ~0.1 ms per pack)
+  static_assert(kRows == 128, "two rows per lane");
+  int t0 = 0, t1 = 0;
+  for (int k0 = 0; k0 < nk; k0 += 8) {
+    int v0[8], v1[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int32_t* h = H + int64_t(min(k0 + u, nk - 1)) * (kRows + 1);
+      v0[u] = h[lane];
+      v1[u] = h[lane + 64];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (k0 + u < nk) {
+        c[lane * nk + k0 + u] = uint8_t(v0[u]);
+        c[(lane + 64) * nk + k0 + u] = uint8_t(v1[u]);
+        t0 += v0[u];
+        t1 += v1[u];
+      }
   }
+  tot[lane] = t0;
+  tot[lane + 64] = t1;
   for (int j = lane; j < kWaves * nk; j += 64) L[j] = 0;
   __syncthreads();
   {
-    for (int i = lane; i < kRows; i += 64) {
-      int t = 0;
-      for (int k = 0; k < nk; ++k) t += c[i * nk + k];
-      tot[i] = t;
-    }
-    __syncthreads();
     int rk[2];
     for (int h = 0; h < 2; ++h) {
       const int i = lane + 64 * h, ti = tot[i];
@@ -715,9 +728,107 @@ __global__ __launch_bounds__(64) void slab_balance_kernel(int32_t* __restrict__ 
     perm[int64_t(g) * kRows + sl] = r < n_rows ? r : -1;
     if (r < n_rows) inv[r] = sl;
   }
-  for (int64_t j = lane; j < int64_t(kRows) * nk; j += 64) {
-    const int i = int(j / nk), k = int(j % nk);
-    H[int64_t(k) * (kRows + 1) + slot_of[i]] = c[j];
+  for (int h = 0; h < 2; ++h) {
+    const int i = lane + 64 * h, sl = slot_of[i];
+    for (int k = 0; k < nk; ++k) H[int64_t(k) * (kRows + 1) + sl] = c[i * nk + k];
+  }
+}
+
+// The same greedy packing for nk <= NKM (x_rows <= 64 NKM) with the wave loads
+// in registers: lanes 0..15 are the 16 waves, each holding its NKM chunk loads,
+// so a step is one LDS read of the row's counts (four per word), the sums of
+// squares in registers, a DPP min over the 16 lanes and one update -- no
+// barrier, no LDS round trip for the loads.  The row order and the keys
+// ((part << 4) | wave, smallest wins) are slab_balance_kernel's: same slots.
+template <int NKM>
+__global__ __launch_bounds__(64) void slab_balance_reg_kernel(int32_t* __restrict__ hdr, int n_rows, int nk,
+                                                              int32_t* __restrict__ perm, int32_t* __restrict__ inv) {
+  static_assert(NKM % 4 == 0 && kRows == 128 && kWaves == 16, "layout");
+  __shared__ __attribute__((aligned(16))) uint8_t c[kRows * NKM];  // counts, row-major, zero past nk
+  __shared__ int tot[kRows];                                      // row totals, then the order
+  __shared__ int slot_of[kRows];
+  const int g = blockIdx.x, lane = threadIdx.x;
+  int32_t* H = hdr + int64_t(g) * nk * (kRows + 1);
+  int t0 = 0, t1 = 0;
+#pragma unroll
+  for (int k0 = 0; k0 < NKM; k0 += 8) {
+    int v0[8], v1[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int32_t* h = H + int64_t(min(k0 + u, nk - 1)) * (kRows + 1);
+      v0[u] = k0 + u < nk ? h[lane] : 0;
+      v1[u] = k0 + u < nk ? h[lane + 64] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      c[lane * NKM + k0 + u] = uint8_t(v0[u]);
+      c[(lane + 64) * NKM + k0 + u] = uint8_t(v1[u]);
+      t0 += v0[u];
+      t1 += v1[u];
+    }
+  }
+  tot[lane] = t0;
+  tot[lane + 64] = t1;
+  __syncthreads();
+  int rk0 = 0, rk1 = 0;
+  for (int j = 0; j < kRows; ++j) {
+    const int tj = tot[j];
+    rk0 += (tj > t0) | ((tj == t0) & (j < lane));
+    rk1 += (tj > t1) | ((tj == t1) & (j < lane + 64));
+  }
+  __syncthreads();
+  tot[rk0] = lane;  // tot becomes order[]: rows by rank
+  tot[rk1] = lane + 64;
+  __syncthreads();
+  const int w = lane & (kWaves - 1);
+  const int ord0 = tot[lane], ord1 = tot[lane + 64];  // the order in registers (lane s % 64)
+  int L[NKM];
+#pragma unroll
+  for (int k = 0; k < NKM; ++k) L[k] = 0;
+  int filled = 0;
+  // the counts of step s + 1's row are read while step s decides (the order
+  // does not depend on the decisions)
+  auto row_words = [&](int s, uint32_t (&wd)[NKM / 4]) {
+    const int i = __builtin_amdgcn_readlane(s < 64 ? ord0 : ord1, s & 63);
+    const uint32_t* cw = reinterpret_cast<const uint32_t*>(c + i * NKM);
+#pragma unroll
+    for (int q = 0; q < NKM / 4; ++q) wd[q] = cw[q];
+    return i;
+  };
+  uint32_t wnext[NKM / 4];
+  int inext = row_words(0, wnext);
+  for (int s = 0; s < kRows; ++s) {
+    const int i = inext;
+    uint32_t words[NKM / 4];
+#pragma unroll
+    for (int q = 0; q < NKM / 4; ++q) words[q] = wnext[q];
+    if (s + 1 < kRows) inext = row_words(s + 1, wnext);
+    int part = 0;
+#pragma unroll
+    for (int k = 0; k < NKM; ++k) {
+      const int ck = int((words[k >> 2] >> (8 * (k & 3))) & 255u);
+      part += ck * (2 * L[k] + ck);
+    }
+    int key = (lane < kWaves && filled < kRW) ? (part << 4) | w : INT32_MAX;
+    // min over lanes 0..15 (one DPP row): shifts in from outside the row read INT32_MAX
+    key = min(key, __builtin_amdgcn_update_dpp(INT32_MAX, key, 0x111, 0xf, 0xf, false));  // row_shr:1
+    key = min(key, __builtin_amdgcn_update_dpp(INT32_MAX, key, 0x112, 0xf, 0xf, false));  // row_shr:2
+    key = min(key, __builtin_amdgcn_update_dpp(INT32_MAX, key, 0x114, 0xf, 0xf, false));  // row_shr:4
+    key = min(key, __builtin_amdgcn_update_dpp(INT32_MAX, key, 0x118, 0xf, 0xf, false));  // row_shr:8
+    const int wb = __builtin_amdgcn_readlane(key, kWaves - 1) & (kWaves - 1);
+    if (lane == wb) {
+#pragma unroll
+      for (int k = 0; k < NKM; ++k) L[k] += int((words[k >> 2] >> (8 * (k & 3))) & 255u);
+      slot_of[i] = wb * kRW + filled;
+      ++filled;
+    }
+  }
+  __syncthreads();
+  for (int h = 0; h < 2; ++h) {
+    const int i = lane + 64 * h, r = g * kRows + i, sl = slot_of[i];
+    perm[int64_t(g) * kRows + sl] = r < n_rows ? r : -1;
+    if (r < n_rows) inv[r] = sl;
+    for (int k = 0; k < nk; ++k) H[int64_t(k) * (kRows + 1) + sl] = c[i * NKM + k];
   }
 }
 
@@ -895,10 +1006,18 @@ extern "C" int dol_csr_slab_pack(const int32_t* rowptr, const int32_t* col, cons
   int32_t* inv = perm + n_rg * kRows;
   const int bal = balance && nk <= kBalMaxNk;  // beyond: slots in row order
   const size_t bal_lds = bal ? size_t(kWaves) * nk * 4 + 2 * kRows * 4 + size_t(kRows) * nk : 16;
-  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(slab_balance_kernel),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(bal_lds));
-  hipLaunchKernelGGL(slab_balance_kernel, dim3(static_cast<unsigned>(n_rg)), dim3(64), bal_lds, s, hdr, n_rows, nk,
-                     perm, inv, bal);
+  if (bal && nk <= 16)
+    hipLaunchKernelGGL(slab_balance_reg_kernel<16>, dim3(static_cast<unsigned>(n_rg)), dim3(64), 0, s, hdr, n_rows, nk,
+                       perm, inv);
+  else if (bal && nk <= 64)
+    hipLaunchKernelGGL(slab_balance_reg_kernel<64>, dim3(static_cast<unsigned>(n_rg)), dim3(64), 0, s, hdr, n_rows, nk,
+                       perm, inv);
+  else {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(slab_balance_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(bal_lds));
+    hipLaunchKernelGGL(slab_balance_kernel, dim3(static_cast<unsigned>(n_rg)), dim3(64), bal_lds, s, hdr, n_rows, nk,
+                       perm, inv, bal);
+  }
   hipLaunchKernelGGL(slab_scan_kernel, dim3(1), dim3(1024), 0, s, hdr, blocks);
   hipLaunchKernelGGL(slab_scatter_kernel, dim3(static_cast<unsigned>(n_rows)), dim3(64), 0, s, rowptr, col, val, nk,
                      inv, hdr, ent, slab_align());
