@@ -81,6 +81,10 @@ struct MlpArgs {
   int update;                    // 0: gradients only (forward_backward)
   int f1_keep;                   // F1 stages W1 / X with the default cache policy (DOL_MLP_F1_KEEP, default 1)
   int dw1_reverse;               // dW1 walks the agents last to first (DOL_MLP_DW1_REVERSE, default 1)
+  // forward phase offset (DOL_MLP_FWD_STAGGER): workgroups lo, lo + step, .. < hi
+  // start `stagger` x s_sleep(127) late, so co-resident workgroups run F1 and
+  // the HBM-idle tail out of step
+  int stagger, stagger_lo, stagger_hi, stagger_step;
 #ifdef DOL_MLP_TRACE
   long long* trace;              // tools/mlp_phase.hip: per-agent phase timestamps
 #endif
@@ -367,6 +371,11 @@ __device__ __forceinline__ void mlp_fused_dw1(const MlpArgs& a, const f4 (&wres)
 template <int NT, int UPD, bool TH, bool AL, int NS = kStages, int PH = 0, int NK = 0>
 __device__ __forceinline__ void mlp_fwd_body(MlpArgs a, float* __restrict__ ws) {
   static_assert(PH != 3 || (NT == 1 && NK > 0 && !TH && !AL && UPD >= 1), "fused step: plain / momentum SGD, one tile per wave");
+  if (a.stagger > 0) {
+    const int bx = int(blockIdx.x);
+    if (bx >= a.stagger_lo && bx < a.stagger_hi && (bx - a.stagger_lo) % a.stagger_step == 0)
+      for (int i = 0; i < a.stagger; ++i) __builtin_amdgcn_s_sleep(127);
+  }
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int B = a.B, d = a.d, h = a.h, c = a.c;
   const int hp = h + 4;  // padded LDS rows: 16-B aligned, rows 4 banks apart
@@ -996,6 +1005,32 @@ extern "C" int dol_mlp_step_f32(float* w, int64_t ldw, float* grad, int64_t ldg,
   static const int dw1_rev = [] { const char* e = getenv("DOL_MLP_DW1_REVERSE"); return e ? atoi(e) : 1; }();
   a.f1_keep = f1_keep;
   a.dw1_reverse = dw1_rev;
+  // r06: the forward's second workgroup slot of every CU (blocks [n_cu, 2 n_cu))
+  // starts ~20 us late, so the two workgroups of a CU run F1 (HBM) and the
+  // HBM-idle tail out of step for the rest of the launch: local step 0.4686-
+  // 0.4696 vs 0.4743-0.4836 ms, three alternating trials, same bits
+  // (tools/mlp_stagger_ab.py, profiles/r06u_mlp_stagger_ab.jsonl); only with
+  // >= 4 n_cu agents (two full rounds of workgroups).  DOL_MLP_FWD_STAGGER =
+  // "count,mode" overrides (read per call; "0" = off; mode 2 = the odd blocks of
+  // [0, 2 n_cu), measured slower)
+  {
+    static const int n_cu = [] {
+      int dev = 0, cu = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cu = 0;
+      return cu;
+    }();
+    const char* e = getenv("DOL_MLP_FWD_STAGGER");  // read per call (A/B in one process)
+    int cnt = (n_cu > 0 && n_agents >= 4 * n_cu) ? 6 : 0, mode = 1;
+    if (e && sscanf(e, "%d,%d", &cnt, &mode) < 1) cnt = 0;
+    if (cnt > 0 && n_cu > 0) {
+      a.stagger = cnt;
+      a.stagger_lo = mode == 2 ? 1 : n_cu;
+      a.stagger_hi = 2 * n_cu;
+      a.stagger_step = mode == 2 ? 2 : 1;
+    }
+  }
   const size_t lds = static_cast<size_t>(dol_mlp_step_lds_bytes(B, h, c));
   if (lds > 160 * 1024) return fail(DOL_EINVAL, "dol_mlp_step_f32: %zu B of LDS per agent exceeds 160 KiB", lds);
   const dim3 grid(static_cast<unsigned>(n_agents)), block(kThreads);

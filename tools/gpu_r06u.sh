@@ -14,3 +14,5 @@ print('value', d['value'], 'frac', d['roofline']['frac'])
 print('er_exact_mix', d['er_exact_mix']['ms_per_round'], d['er_exact_mix']['mix_ms'])
 print('config5', d['config5_round']['ms_per_round'], d['config5_round']['phase_ms'])
 "
+timeout -k 10 300 python -u tools/mlp_stagger_ab.py > $O/stagger.jsonl 2> $O/stagger.err || { echo "stagger failed"; tail -10 $O/stagger.err; exit 1; }
+cat $O/stagger.jsonl
