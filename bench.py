@@ -29,6 +29,7 @@ config-5 round (ER draw + device Neighbors + fused MLP local step + exact mix).
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -45,8 +46,16 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 def _log(msg: str) -> None:
-    """Progress on stderr (stdout carries only the one JSON line)."""
-    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+    """Progress on stderr (stdout carries only the one JSON line), with the
+    device's free memory once CUDA is up (a leg that OOMs names what held it)."""
+    free = ""
+    try:
+        if torch.cuda.is_initialized():
+            f, _ = torch.cuda.mem_get_info()
+            free = f" [free {f / 2**30:.1f} GiB, torch {torch.cuda.memory_allocated() / 2**30:.1f} GiB]"
+    except Exception:  # noqa: BLE001 -- diagnostics only
+        pass
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}{free}", file=sys.stderr, flush=True)
 
 
 METRIC = "consensus rounds/sec at 8192 agents x 1M params (1/8 GPU) + % of HBM peak"
@@ -982,6 +991,7 @@ def main():
     if not args.no_copy:
         calib = copy_peak(device, ring.x, ring.y, P)
     del ring.x, ring.y
+    gc.collect()  # the legs' banks may sit in reference cycles: release their mapped blocks now
     torch.cuda.empty_cache()
     _log("calibration done")
     pd_round = None
