@@ -977,6 +977,7 @@ extern "C" int dol_mix_csr_slab_f32(const float* X, int64_t ldx, int32_t x_rows,
   else if (probe == 4) launch(csr_slab_kernel<4>);
   else if (probe == 5) launch(csr_slab_kernel<5>);
   else if (probe == 6) launch(csr_slab_kernel<6>);
+  else if (probe == 7) launch(csr_slab_kernel<3, false, 2>);  // the asm stream without the chunk barrier (timing bound; wrong bits)
   else if (slab_align() == 4) launch(csr_slab_kernel<0, true>);
   else {
     int v = g_slab_variant.load(std::memory_order_relaxed);
