@@ -184,7 +184,9 @@ SLAB_ZERO_OFFSET = 64 * 1024  # csr_slab.hip kZeroRel: the zero piece after each
 
 
 @pytest.mark.parametrize("balance", [False, True])
-@pytest.mark.parametrize("n,p", [(200, 0.2), (300, 0.05), (1024, 0.1)])
+@pytest.mark.parametrize("n,p", [(200, 0.2), (300, 0.05), (1024, 0.1),
+                                 (2000, 0.05),    # 32 chunks: the 64-chunk register packing kernel
+                                 (4200, 0.01)])   # 66 chunks: the LDS packing kernel
 def test_slab_pack_matches_host(n, p, balance, gpu):
     csr = er_csr(n, p, seed=3, empty_rows=(7,))
     plan = G.MixingPlan(csr, gpu, slab=True)
