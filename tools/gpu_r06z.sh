@@ -2,7 +2,7 @@
 # r06z: the final tree -- GPU suite, smoke, the N = 1 bench line, and the bench
 # under rocprofv3 (kernel trace + FETCH_SIZE / WRITE_SIZE passes, summarised)
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/r06z; mkdir -p $O
+O=$R/gpurun_out/${RUN:-r06z}; mkdir -p $O
 cd $R
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/suite.txt 2>&1 || { echo "suite failed"; tail -40 $O/suite.txt; exit 1; }
 tail -1 $O/suite.txt
@@ -16,4 +16,4 @@ print('er_exact_mix', d['er_exact_mix']['ms_per_round'], d['er_exact_mix']['mix_
 print('config5', d['config5_round']['ms_per_round'], d['config5_round']['phase_ms'])
 print('split3', d['dense_er_mix']['bf16_mfma_util'])
 "
-OUT=gpurun_out/r06z_prof bash tools/profile_cmd_summary.sh bench.py --steps 20 --no-cpu || { echo "profile failed"; exit 1; }
+[ -n "$NO_PROF" ] || { export DOL_BANK_ALLOC=torch; OUT=gpurun_out/${RUN:-r06z}_prof bash tools/profile_cmd_summary.sh bench.py --steps 20 --no-cpu --map-ring 0 || { echo "profile failed"; exit 1; }; }
