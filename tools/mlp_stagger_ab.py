@@ -18,6 +18,8 @@ from dolhip.bank import AgentBank  # noqa: E402
 from dolhip.mlp import BatchedMLP, mlp_layout  # noqa: E402
 
 SETTINGS = ["0", "4,1", "6,1", "8,1", "6,2"]
+if os.environ.get("DOL_STAGGER_SETTINGS"):
+    SETTINGS = os.environ["DOL_STAGGER_SETTINGS"].split(";")
 
 
 def main():
