@@ -745,7 +745,8 @@ def er_exact_mix_round(device, N: int = 1024, P: int = 101770, reps: int = 10):
     def draw():
         st["r"] += 1
         W = G.erdos_renyi_stochastic_hip(N, 0.1, 2028 * 1000003 + st["r"], device, out=Wbuf)
-        st["plan"] = G.MixingPlan.from_dense(W, dense_kernel="csr", reuse=st["plan"])
+        st["plan"] = G.MixingPlan.from_dense(W, dense_kernel="csr", reuse=st["plan"],
+                                           balance=True)  # the config-5 product path's pack
     draw()
     st["plan"].apply(X, Y, P=P)
     _warm(lambda: (draw(), st["plan"].apply(X, Y, P=P)))
@@ -840,7 +841,7 @@ def config5_round(device, N: int = 1024, reps: int = 10):
         st["r"] += 1
         rec("graph", 0)
         W = G.erdos_renyi_stochastic_hip(N, 0.1, 2028 * 1000003 + st["r"], device, out=Wbuf)
-        st["plan"] = G.MixingPlan.from_dense(W, dense_kernel="csr", reuse=st["plan"])
+        st["plan"] = G.MixingPlan.from_dense(W, dense_kernel="csr", reuse=st["plan"], balance=True)  # as the product path packs
         rec("graph", 1)
         rec("local", 0)
         mlp.step(X, y, lr=0.05, momentum=0.5, first_step=False)

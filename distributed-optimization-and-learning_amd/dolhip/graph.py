@@ -382,15 +382,18 @@ class MixingPlan:
             return float((self.W > 0).sum().item()) / max(1, self.W.numel())
         return self.csr.nnz / max(1, self.csr.n_rows * self.csr.n_cols)
 
-    # from_dense(csr) deals rows to the slab kernel's waves by their per-chunk
-    # loads (csr_slab_pack balance=True) up to this many X rows (64 chunks: the
-    # register-resident packing kernel, ~0.02 ms at 1024 agents, where the
-    # balanced mix runs ~2-3 % faster; beyond, the LDS kernel costs more than it saves)
+    # from_dense(csr, balance=True) deals rows to the slab kernel's waves by their
+    # per-chunk loads (csr_slab_pack balance=True) up to this many X rows (64
+    # chunks: the register-resident packing kernel, ~0.04 ms at 1024 agents,
+    # where the balanced mix runs ~2-3 % faster; beyond, the LDS kernel costs
+    # more than it saves).  Worth it where the pack overlaps other work (the
+    # config-5 round builds the next plan on a side stream during the local
+    # step); a plan built and mixed back to back is faster unbalanced.
     BALANCE_MAX_X_ROWS = 4096
 
     @classmethod
     def from_dense(cls, W: torch.Tensor, dense_kernel: str = "split3",
-                   reuse: Optional["MixingPlan"] = None, balance: Optional[bool] = None) -> "MixingPlan":
+                   reuse: Optional["MixingPlan"] = None, balance: bool = False) -> "MixingPlan":
         """A plan straight from a device W (no host round trip; e.g. a per-round
         erdos_renyi_stochastic_hip draw).  dense_kernel 'split3' / 'f32': a
         'dense' plan on the matrix cores (tolerance path).  dense_kernel 'csr':
@@ -399,8 +402,8 @@ class MixingPlan:
         previous 'csr' plan of the same shape) lends its buffers and is retired
         (mixing with it afterwards raises).  The lent col / val buffers are sized
         n_rows * n_cols (a dense W's worst case), so a reused plan never
-        reallocates whatever the round's W.  balance (None: n_cols <=
-        BALANCE_MAX_X_ROWS): the wave-balanced packing (same bits)."""
+        reallocates whatever the round's W.  balance: the wave-balanced packing
+        (same bits) when n_cols <= BALANCE_MAX_X_ROWS."""
         if W.device.type != "cuda" or W.dtype != torch.float32 or W.dim() != 2:
             raise ValueError("from_dense: expected a 2-D float32 CUDA tensor")
         if dense_kernel not in cls.DENSE_KERNELS + ("csr",):
@@ -422,8 +425,7 @@ class MixingPlan:
                 and (reuse.n_rows, reuse.n_cols) == (plan.n_rows, plan.n_cols))
         bufs = (reuse.rowptr, reuse.col, reuse.val) if same else (None, None, None)
         plan.rowptr, plan.col, plan.val = ops.dense_to_csr(plan.W, *bufs)
-        if balance is None:
-            balance = plan.n_cols <= cls.BALANCE_MAX_X_ROWS
+        balance = bool(balance) and plan.n_cols <= cls.BALANCE_MAX_X_ROWS
         plan.ent, plan.hdr = ops.csr_slab_pack(plan.rowptr, plan.col, plan.val, plan.n_cols,
                                                *((reuse.ent, reuse.hdr) if same else (None, None)),
                                                balance=bool(balance))

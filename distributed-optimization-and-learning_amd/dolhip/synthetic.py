@@ -527,7 +527,8 @@ class TimeVaryingMLPGossip:
         with torch.cuda.stream(self._side):
             W = G.erdos_renyi_stochastic_hip(self.N, self.p_edge, self.round_seed(self.rounds), self.device,
                                              out=self._W)
-            self._plan = G.MixingPlan.from_dense(W, dense_kernel="csr", reuse=self._plan)
+            # balanced pack: it runs here, on the side stream, under the local step
+            self._plan = G.MixingPlan.from_dense(W, dense_kernel="csr", reuse=self._plan, balance=True)
         if self.tr is None:
             loss = self.mlp.step(self.X, self.y, lr=self.lr, momentum=self.mu, first_step=(self.rounds == 0))
             self._plan_ready(main)

@@ -316,3 +316,22 @@ def test_slab_8192_agents(gpu, slab_variant):
     ops.mix_csr(Xd, Yg, plan.rowptr, plan.col, plan.val)
     torch.cuda.synchronize()
     assert torch.equal(Yd.view(torch.int32), Yg.view(torch.int32))
+
+
+@pytest.mark.parametrize("balance", [False, True])
+def test_from_dense_plan_balanced_or_not_mixes_bit_exactly(balance, gpu):
+    """MixingPlan.from_dense(W, 'csr', balance=...): the device-built plan, with
+    or without the wave-balanced pack (TimeVaryingMLPGossip packs balanced on
+    its side stream), gives the oracle's bits."""
+    n, P = 300, 1001
+    csr = er_csr(n, 0.2, seed=11)
+    W = np.zeros((n, n), np.float32)
+    for i in range(n):
+        W[i, csr.col[csr.rowptr[i]:csr.rowptr[i + 1]]] = csr.val[csr.rowptr[i]:csr.rowptr[i + 1]]
+    plan = G.MixingPlan.from_dense(torch.as_tensor(W, device=gpu), dense_kernel="csr", balance=balance)
+    X = special_x(n, P, seed=5)
+    ld = -(-P // 4) * 4
+    Xd, Yd = bank_like(X, gpu, ld), bank_like(np.zeros_like(X), gpu, ld)
+    plan.apply(Xd, Yd, P=P)
+    torch.cuda.synchronize()
+    assert bits_equal(Yd[:, :P].cpu().numpy(), oracle.mix_csr(X, csr.rowptr, csr.col, csr.val))
